@@ -1,0 +1,852 @@
+// rvz_engine.hip — batched Reversi env + lockstep reference-semantics PUCT for gfx950 (MI355X),
+// exported through the C-ABI in include/rvz.h.
+//
+// Layout (HBM, per engine of G games):
+//   env    black[G], white[G] (u64), status[G][4] (side, over, winner, passed)
+//   tree   nodes[G][M] {N i32, W f32, P f32, C f32}, meta[G][M] u32, M = 1 + E*S*S,
+//          E = ceil(sims / batch) = expansions per search; node 0 = root, expansion e of a search
+//          owns the child block [1 + e*S*S, 1 + (e+1)*S*S), children in row-major square order.
+//   search path[G][64] i32, pend[G] (queued copies), plen[G], leaf_legal[G] u64, nexp[G]
+//   rng    u[G][64] f64: np.random.random_sample() stream of each game's seed, pos[G]
+//
+// One wavefront per game in every search kernel: lane i owns child i (UCB, expansion) or
+// square i (planes, visits, policy), so a 64-square board is exactly one wave.
+//
+// Exactness notes (mirrored and checked by oracle/rvz_oracle.c, which keeps the literal rules):
+//  * Within a batch every traversal of a game follows the same path (UCB scores are cached and only
+//    invalidated by a backup of that node, mcts.py:99-113,639-640; unvisited children score +inf,
+//    mcts.py:96-97), unless a traversal ends on an already-known terminal, which is backed up at
+//    once (mcts.py:364-366). select therefore walks once per terminal hit plus once for the
+//    queued leaf, and backs the NN value up `copies` times (B sequential fp32 adds).
+//  * Virtual loss is always 0 when a score is computed (every traversal that scores starts from a
+//    balanced tree), so u = c*P*sqrt(Np) / (1 + N).
+//  * value_sum is float32 (NumPy>=2 promotion of the np.float32 NN value); terminal values are
+//    small integers, exact in float32, so one float32 accumulator reproduces the Python mix.
+//  * sqrt(Np) is taken from a host-built table of (float)sqrt((double)n) (math.sqrt then the
+//    float32 cast), so no device sqrt rounding enters the scores.
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rvz.h"
+#include "rvz_rules.hip.h"
+
+using namespace rvz;
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int WPB = 4;            // waves (games) per 256-thread workgroup
+constexpr int PATH_CAP = 64;      // path length limit: ceil(sims / batch) <= 64
+constexpr int RNG_DRAWS = 64;     // random_sample() values per seed (a game has <= 60 plies)
+
+struct Node {
+    int32_t n;   // visit_count
+    float w;     // value_sum
+    float p;     // prior
+    float c;     // cached_ucb; NaN = not cached
+};
+static_assert(sizeof(Node) == 16, "node is one 16-byte load");
+
+// meta word: sq[0:6) turn[6:8) terminal[8] tv[9:11) (0: 0.0, 1: +1.0, 2: -1.0) nchild[11:18) block[18:32)
+__host__ __device__ constexpr uint32_t meta_pack(int sq, int turn) {
+    return (uint32_t)(sq & 63) | ((uint32_t)(turn & 3) << 6);
+}
+__device__ __forceinline__ int m_sq(uint32_t m) { return (int)(m & 63u); }
+__device__ __forceinline__ int m_turn(uint32_t m) { return (int)((m >> 6) & 3u); }
+__device__ __forceinline__ bool m_term(uint32_t m) { return (m >> 8) & 1u; }
+__device__ __forceinline__ float m_tv(uint32_t m) {
+    const uint32_t t = (m >> 9) & 3u;
+    return t == 1u ? 1.0f : (t == 2u ? -1.0f : 0.0f);
+}
+__device__ __forceinline__ int m_nchild(uint32_t m) { return (int)((m >> 11) & 127u); }
+__device__ __forceinline__ int m_block(uint32_t m) { return (int)(m >> 18); }
+
+struct View {  // kernel argument: device pointers + sizes
+    int G, M;
+    float cpuct;
+    uint64_t* black;
+    uint64_t* white;
+    int32_t* status;  // [G][4]
+    Node* nodes;
+    uint32_t* meta;
+    int32_t* path;  // [G][PATH_CAP]
+    int32_t* pend;
+    int32_t* plen;
+    uint64_t* leaf_legal;
+    int32_t* nexp;
+    const float* sqrt_tab;  // [sims + 1]
+    double* rng_u;          // [G][RNG_DRAWS]
+    int32_t* rng_pos;
+    int32_t* err;
+};
+
+enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4 };
+
+__device__ __forceinline__ GameS load_game(const View& v, int g) {
+    GameS s;
+    s.black = v.black[g];
+    s.white = v.white[g];
+    const int4 st = reinterpret_cast<const int4*>(v.status)[g];
+    s.side = st.x; s.over = st.y; s.winner = st.z; s.passed = st.w;
+    return s;
+}
+__device__ __forceinline__ void store_game(const View& v, int g, const GameS& s) {
+    v.black[g] = s.black;
+    v.white[g] = s.white;
+    reinterpret_cast<int4*>(v.status)[g] = make_int4(s.side, s.over, s.winner, s.passed);
+}
+
+// ---- wave primitives --------------------------------------------------------------------------
+__device__ __forceinline__ int wave_sum_i(int x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+__device__ __forceinline__ float wave_max_f(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ float wave_sum_f(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+// First index holding the maximum: Python's `if score > best_score` scan over the children dict
+// (mcts.py:423-428). NaN never wins (NaN > x is False); -0.0 ties +0.0.
+__device__ __forceinline__ int wave_argmax_first(float s, bool valid, int lane) {
+    const float z = (s == 0.0f) ? 0.0f : s;
+    const uint32_t b = __float_as_uint(z);
+    uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    if (!valid || isnan(s)) key = 0u;
+    uint64_t k = ((uint64_t)key << 32) | (uint32_t)(63 - lane);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t other = __shfl_xor(k, o);
+        k = other > k ? other : k;
+    }
+    return 63 - (int)(uint32_t)(k & 0xffffffffu);
+}
+
+// ---- backup (mcts.py:625-640): lane j updates path node plen-1-j; `copies` sequential adds ----
+__device__ __forceinline__ void backup_path(Node* nodes, int mypath, int plen, float value,
+                                            int copies, int lane) {
+    // order this wave's earlier node stores (UCB caches) before the read-modify-write below
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    const int j = plen - 1 - lane;  // lane's path index counted from the root
+    const int nid = __shfl(mypath, j < 0 ? 0 : j);
+    if (lane < plen) {
+        const float sv = (lane & 1) ? -value : value;  // sign = +1 at the leaf, then alternates
+        Node nd = nodes[nid];
+        float w = nd.w;
+        for (int k = 0; k < copies; ++k) w = w + sv;
+        nd.n += copies;
+        nd.w = w;
+        nd.c = __int_as_float(0x7fc00000);  // del cached_ucb
+        nodes[nid] = nd;
+    }
+}
+
+// UCB of an expanded child whose score is not cached (mcts.py:102-114); turn_c = child's turn.
+__device__ __forceinline__ float ucb_score(const Node& c, int parent_n, int turn_c, float cpuct,
+                                           const float* sqrt_tab) {
+    float u = cpuct * c.p;
+    u = u * sqrt_tab[parent_n];
+    u = u / (float)(1 + c.n);
+    float q = c.w / (float)(c.n > 1 ? c.n : 1);
+    if (turn_c != 1) q = -q;
+    return q + u;
+}
+
+// ---- search kernels -----------------------------------------------------------------------------
+// select: mcts.py:348-386 for one batch of `bsz` traversals + _process_batch pass 1 (:561-585).
+template <int BS, typename XT>
+__global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* __restrict__ leaf_x,
+                                                int32_t* __restrict__ need) {
+    constexpr int NSQ = Geo<BS>::NSQ;
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (g >= v.G) return;
+    Node* nodes = v.nodes + (size_t)g * v.M;
+    uint32_t* meta = v.meta + (size_t)g * v.M;
+    const GameS root = load_game(v, g);
+    uint32_t root_meta;
+    if (first) {  // new root (mcts.py:334-341): prior 1.0, turn = side to move
+        root_meta = meta_pack(0, root.side);
+        if (lane == 0) {
+            Node r;
+            r.n = 0; r.w = 0.0f; r.p = 1.0f; r.c = __int_as_float(0x7fc00000);
+            nodes[0] = r;
+            meta[0] = root_meta;
+            v.nexp[g] = 0;
+        }
+    } else {
+        root_meta = meta[0];
+    }
+    int copies = 0, plen = 0, mypath = 0;
+    if (!root.over) {
+        int remaining = bsz;
+        for (;;) {
+            GameS sim = root;
+            int node = 0, depth = 0;
+            uint32_t m = root_meta;
+            mypath = 0;  // lane 0 holds the root
+            for (;;) {
+                const int nch = m_nchild(m);
+                if (m_term(m) || nch == 0) break;  // while node.expanded() and not terminal
+                const int parent_n = nodes[node].n;
+                const int base = 1 + m_block(m) * NSQ;
+                float score = 0.0f;
+                if (lane < nch) {
+                    const Node c = nodes[base + lane];
+                    if (c.n == 0) {
+                        score = INFINITY;
+                    } else if (!isnan(c.c)) {
+                        score = c.c;
+                    } else {
+                        score = ucb_score(c, parent_n, 3 - m_turn(m), v.cpuct, v.sqrt_tab);
+                        nodes[base + lane].c = score;
+                    }
+                }
+                const int ci = wave_argmax_first(score, lane < nch, lane);
+                node = base + ci;
+                m = meta[node];
+                make_move<BS>(sim, m_sq(m));
+                ++depth;
+                if (depth >= PATH_CAP) {  // unreachable when ceil(sims/batch) <= 64 (checked)
+                    if (lane == 0) atomicOr(v.err, ERR_PATH);
+                    depth = PATH_CAP - 1;
+                    break;
+                }
+                if (lane == depth) mypath = node;
+            }
+            if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
+                backup_path(nodes, mypath, depth + 1, m_tv(m), 1, lane);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                if (--remaining == 0) break;
+                continue;
+            }
+            // pass 1: valid moves of the leaf's simulated game
+            const uint64_t V = legal<BS>(mine(sim), theirs(sim));
+            if (V == 0ull) {  // terminal, BLACK-absolute value from get_winner() (mcts.py:567-579)
+                const int w = sim.over ? sim.winner : -1;
+                const uint32_t code = w == 1 ? 1u : (w == 2 ? 2u : 0u);
+                if (lane == 0) meta[node] = m | (1u << 8) | (code << 9);
+                backup_path(nodes, mypath, depth + 1, w == 1 ? 1.0f : (w == 2 ? -1.0f : 0.0f),
+                            remaining, lane);
+                break;
+            }
+            // queue `remaining` identical copies for the NN: encode get_canonical_state() planes
+            copies = remaining;
+            plen = depth + 1;
+            if (lane < NSQ) {
+                XT* row = leaf_x + (size_t)g * 3 * NSQ;
+                const uint64_t P = mine(sim), O = theirs(sim);
+                row[lane] = (XT)(float)((P >> lane) & 1ull);
+                row[NSQ + lane] = (XT)(float)((O >> lane) & 1ull);
+                row[2 * NSQ + lane] = (XT)(float)((V >> lane) & 1ull);
+            }
+            if (lane < plen) v.path[g * PATH_CAP + lane] = mypath;
+            if (lane == 0) v.leaf_legal[g] = V;
+            break;
+        }
+    }
+    if (lane == 0) {
+        need[g] = copies;
+        v.pend[g] = copies;
+        v.plen[g] = plen;
+    }
+}
+
+// expand + backup: _process_batch pass 2 (mcts.py:600-623) and MCTSNode.expand (:141-161).
+template <int BS>
+__global__ __launch_bounds__(256) void k_expand_backup(View v, const float* __restrict__ policy,
+                                                       int is_logits,
+                                                       const float* __restrict__ value) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (g >= v.G) return;
+    const int copies = v.pend[g];
+    if (copies == 0) return;
+    const int plen = v.plen[g];
+    const int mypath = lane < plen ? v.path[g * PATH_CAP + lane] : 0;
+    const int leaf = __shfl(mypath, plen - 1);
+    Node* nodes = v.nodes + (size_t)g * v.M;
+    uint32_t* meta = v.meta + (size_t)g * v.M;
+    const uint64_t V = v.leaf_legal[g];
+    const float* row = policy + (size_t)g * NPOL;
+    float prob = lane < NSQ ? row[lane] : 0.0f;
+    if (is_logits) {  // F.softmax(policy_logits, dim=1) over all S*S+1 outputs (mcts.py:596)
+        const float xpass = row[NSQ];
+        const float mx = fmaxf(wave_max_f(lane < NSQ ? prob : -INFINITY), xpass);
+        const float e = lane < NSQ ? expf(prob - mx) : 0.0f;
+        const float denom = wave_sum_f(e) + expf(xpass - mx);
+        prob = e / denom;
+    }
+    const uint32_t lm = meta[leaf];
+    const int e = v.nexp[g];
+    const int base = 1 + e * NSQ;
+    if (base + NSQ > v.M) {
+        if (lane == 0) atomicOr(v.err, ERR_POOL);
+        return;
+    }
+    if (lane < NSQ && ((V >> lane) & 1ull)) {
+        const int idx = __popcll(V & ((1ull << lane) - 1ull));
+        Node c;
+        c.n = 0; c.w = 0.0f; c.p = prob; c.c = __int_as_float(0x7fc00000);
+        nodes[base + idx] = c;
+        meta[base + idx] = meta_pack(lane, 3 - m_turn(lm));
+    }
+    if (lane == 0) {
+        meta[leaf] = lm | ((uint32_t)__popcll(V) << 11) | ((uint32_t)e << 18);
+        v.nexp[g] = e + 1;
+        v.pend[g] = 0;
+    }
+    backup_path(nodes, mypath, plen, value[g], copies, lane);
+}
+
+// Dense visit count of square `lane` at the root: the root's children are the set bits of the
+// root board's legal mask in ascending order (expand inserts them row-major).
+template <int BS>
+__device__ __forceinline__ int root_visits(const View& v, int g, const GameS& root, int lane) {
+    constexpr int NSQ = Geo<BS>::NSQ;
+    const Node* nodes = v.nodes + (size_t)g * v.M;
+    const uint32_t m0 = v.meta[(size_t)g * v.M];
+    const int nch = m_nchild(m0);
+    if (nch == 0 || lane >= NSQ) return 0;
+    const uint64_t V = legal<BS>(mine(root), theirs(root));
+    if (!((V >> lane) & 1ull)) return 0;
+    const int idx = __popcll(V & ((1ull << lane) - 1ull));
+    return nodes[1 + m_block(m0) * NSQ + idx].n;
+}
+
+template <int BS>
+__global__ __launch_bounds__(256) void k_visits(View v, int32_t* __restrict__ out) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (g >= v.G) return;
+    const GameS root = load_game(v, g);
+    const int n = root_visits<BS>(v, g, root, lane);
+    if (lane < NSQ) out[(size_t)g * NPOL + lane] = n;
+    if (lane == 0) out[(size_t)g * NPOL + NSQ] = 0;  // no pass child is ever created
+}
+
+// numpy `arr ** e` for float64 (fast_scalar_power paths, else pow).
+__device__ __forceinline__ double np_power(double x, double e) {
+    if (e == 1.0) return x;
+    if (e == 2.0) return x * x;
+    if (e == 0.5) return sqrt(x);
+    if (e == -1.0) return 1.0 / x;
+    if (e == 0.0) return 1.0;
+    return pow(x, e);
+}
+
+// np.sum over [t_0 .. t_{NSQ-1}, tpass] in numpy's pairwise order (8 accumulators, n <= 128).
+template <int NPOL>
+__device__ __forceinline__ double np_pairwise_sum(double t, double tpass) {
+    static_assert(NPOL >= 8 && NPOL <= 128, "pairwise_sum block");
+    constexpr int NMAIN = NPOL - NPOL % 8;
+    auto at = [&](int i) -> double { return i == NPOL - 1 ? tpass : __shfl(t, i); };
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = at(j);
+    for (int i = 8; i < NMAIN; i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += at(i + j);
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int i = NMAIN; i < NPOL; ++i) res += at(i);
+    return res;
+}
+
+// act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action).
+template <int BS>
+__global__ __launch_bounds__(256) void k_act(View v, double temperature, const double* __restrict__ uo,
+                                             int apply, int32_t* __restrict__ out_idx,
+                                             double* __restrict__ out_p) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (g >= v.G) return;
+    GameS gm = load_game(v, g);
+    double* prow = out_p + (size_t)g * NPOL;
+    if (gm.over) {
+        if (lane < NSQ) prow[lane] = 0.0;
+        if (lane == 0) { prow[NSQ] = 0.0; out_idx[g] = -2; }
+        return;
+    }
+    const int n = root_visits<BS>(v, g, gm, lane);
+    const int total = wave_sum_i(n);
+    double p = (lane < NSQ && total > 0) ? (double)n / (double)total : 0.0;
+    double ppass = 0.0;
+    if (temperature > 0.0 && __any(p != 0.0)) {
+        const double ex = 1.0 / temperature;
+        const double t = lane < NSQ ? np_power(p, ex) : 0.0;
+        const double tp = np_power(0.0, ex);
+        const double s = np_pairwise_sum<NPOL>(t, tp);
+        p = t / s;
+        ppass = tp / s;
+    }
+    const bool all_zero = !__any(lane < NSQ && p != 0.0) && ppass == 0.0;
+    int idx;
+    if (temperature == 0.0 || all_zero) {  // np.argmax: first maximum
+        double best = ppass;  // compared last: a square wins ties
+        int bi = NSQ;
+        for (int i = NSQ - 1; i >= 0; --i) {
+            const double pi = __shfl(p, i);
+            if (pi >= best) { best = pi; bi = i; }
+        }
+        idx = bi;
+    } else {  // np.random.choice(NPOL, p=p): cumsum, /= last, searchsorted(u, 'right')
+        double u;
+        if (uo) {
+            u = uo[g];
+        } else {
+            const int pos = v.rng_pos[g];
+            if (pos >= RNG_DRAWS) {
+                if (lane == 0) atomicOr(v.err, ERR_RNG);
+                u = 0.0;
+            } else {
+                u = v.rng_u[(size_t)g * RNG_DRAWS + pos];
+            }
+            if (lane == 0) v.rng_pos[g] = pos + 1;
+        }
+        double acc = 0.0;  // cdf[-1]: the same sequential adds as p.cumsum()
+        for (int i = 0; i < NPOL; ++i) acc += (i < NSQ) ? __shfl(p, i) : ppass;
+        const double last = acc;
+        acc = 0.0;
+        idx = 0;
+        for (int i = 0; i < NPOL; ++i) {
+            acc += (i < NSQ) ? __shfl(p, i) : ppass;
+            if (acc / last <= u) idx = i + 1;  // count of cdf entries <= u
+        }
+    }
+    if (lane < NSQ) prow[lane] = p;
+    if (lane == 0) {
+        prow[NSQ] = ppass;
+        out_idx[g] = idx;
+    }
+    if (apply) {
+        make_move<BS>(gm, idx == NSQ ? -1 : idx);  // (row, col) = (-1, -1) for the pass index
+        if (lane == 0) store_game(v, g, gm);
+    }
+}
+
+// reset: new game (board.py:25-39) + np.random.seed(seed) random_sample() stream.
+template <int BS>
+__global__ __launch_bounds__(256) void k_reset(View v, const uint32_t* __restrict__ seeds,
+                                               const uint8_t* __restrict__ mask) {
+    __shared__ uint32_t key[WPB][624];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = blockIdx.x * WPB + wid;
+    if (g >= v.G) return;
+    if (mask && !mask[g]) return;
+    uint32_t* k = key[wid];
+    if (lane == 0) {  // mt19937_seed (init_genrand): inherently sequential
+        uint32_t s = seeds[g];
+        for (int pos = 0; pos < 624; ++pos) {
+            k[pos] = s;
+            s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(pos + 1);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    // First generation: words 0..127 only need the initial key (i + 397 < 624 for i < 227).
+    auto word = [&](int i) -> uint32_t {
+        const uint32_t y = (k[i] & 0x80000000u) | (k[i + 1] & 0x7fffffffu);
+        uint32_t x = k[i + 397] ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+        x ^= (x >> 11);
+        x ^= (x << 7) & 0x9d2c5680u;
+        x ^= (x << 15) & 0xefc60000u;
+        x ^= (x >> 18);
+        return x;
+    };
+    const uint32_t a = word(2 * lane) >> 5, b = word(2 * lane + 1) >> 6;
+    v.rng_u[(size_t)g * RNG_DRAWS + lane] = ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+    if (lane == 0) {
+        GameS s;
+        s.black = Geo<BS>::START_BLACK;
+        s.white = Geo<BS>::START_WHITE;
+        s.side = 1; s.over = 0; s.winner = -1; s.passed = 0;
+        store_game(v, g, s);
+        v.rng_pos[g] = 0;
+        v.pend[g] = 0;
+    }
+}
+
+// ---- board kernels on caller arrays (one thread per board) --------------------------------------
+template <int BS>
+__global__ void k_board_legal(int n, const uint64_t* __restrict__ black,
+                              const uint64_t* __restrict__ white, const int32_t* __restrict__ status,
+                              uint64_t* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int side = status[4 * i];
+    const uint64_t P = side == 1 ? black[i] : white[i], O = side == 1 ? white[i] : black[i];
+    out[i] = legal<BS>(P, O);
+}
+
+template <int BS>
+__global__ void k_board_apply(int n, uint64_t* __restrict__ black, uint64_t* __restrict__ white,
+                              int32_t* __restrict__ status, const int32_t* __restrict__ sq,
+                              int32_t* __restrict__ ok) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    GameS s;
+    s.black = black[i];
+    s.white = white[i];
+    const int4 st = reinterpret_cast<const int4*>(status)[i];
+    s.side = st.x; s.over = st.y; s.winner = st.z; s.passed = st.w;
+    const bool r = make_move<BS>(s, sq[i]);
+    if (r) {
+        black[i] = s.black;
+        white[i] = s.white;
+        reinterpret_cast<int4*>(status)[i] = make_int4(s.side, s.over, s.winner, s.passed);
+    }
+    if (ok) ok[i] = r ? 1 : 0;
+}
+
+template <int BS>
+__global__ void k_board_canonical(int n, const uint64_t* __restrict__ black,
+                                  const uint64_t* __restrict__ white,
+                                  const int32_t* __restrict__ status, float* __restrict__ out) {
+    constexpr int NSQ = Geo<BS>::NSQ;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / NSQ, s = t % NSQ;
+    if (i >= n) return;
+    const int side = status[4 * i];
+    const uint64_t P = side == 1 ? black[i] : white[i], O = side == 1 ? white[i] : black[i];
+    const uint64_t V = legal<BS>(P, O);
+    float* row = out + (size_t)i * 3 * NSQ;
+    row[s] = (float)((P >> s) & 1ull);
+    row[NSQ + s] = (float)((O >> s) & 1ull);
+    row[2 * NSQ + s] = (float)((V >> s) & 1ull);
+}
+
+}  // namespace
+
+// =================================================================================================
+// host side
+// =================================================================================================
+struct rvz_engine {
+    rvz_config cfg;
+    int BS, NSQ, NPOL, E, M;
+    hipStream_t stream = nullptr;
+    int next_batch = 0;  // batches issued in the current search
+    int searching = 0;
+    int64_t counters[2] = {0, 0};
+    View v;
+    std::vector<void*> allocs;
+    std::string err;
+};
+
+static thread_local std::string g_create_error;
+
+#define RVZ_HIP(call, e)                                                                   \
+    do {                                                                                   \
+        hipError_t _s = (call);                                                            \
+        if (_s != hipSuccess) {                                                            \
+            (e)->err = std::string(#call) + ": " + hipGetErrorString(_s);                  \
+            return RVZ_EHIP;                                                               \
+        }                                                                                  \
+    } while (0)
+
+static int launch_check(rvz_engine* e, const char* what) {
+    hipError_t s = hipGetLastError();
+    if (s != hipSuccess) {
+        e->err = std::string(what) + ": " + hipGetErrorString(s);
+        return RVZ_EHIP;
+    }
+    e->counters[1] += 1;
+    return RVZ_OK;
+}
+
+static int grid_games(int G) { return (G + WPB - 1) / WPB; }
+
+template <typename T>
+static T* dalloc(rvz_engine* e, size_t count) {
+    void* p = nullptr;
+    if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) p = nullptr;
+    e->allocs.push_back(p);
+    return static_cast<T*>(p);
+}
+
+extern "C" {
+
+int rvz_version(void) { return 1; }
+
+const char* rvz_last_error(const rvz_engine* e) {
+    return e ? e->err.c_str() : g_create_error.c_str();
+}
+
+int rvz_create(const rvz_config* cfg, rvz_engine** out) {
+    if (!cfg || !out) { g_create_error = "null argument"; return RVZ_EINVAL; }
+    *out = nullptr;
+    const int bs = cfg->board_size;
+    if (bs != 8 && bs != 6) { g_create_error = "board_size must be 8 or 6"; return RVZ_EINVAL; }
+    if (cfg->n_games <= 0 || cfg->num_simulations <= 0 || cfg->batch_size <= 0) {
+        g_create_error = "n_games, num_simulations and batch_size must be positive";
+        return RVZ_EINVAL;
+    }
+    const int E = (cfg->num_simulations + cfg->batch_size - 1) / cfg->batch_size;
+    if (E > PATH_CAP) {
+        g_create_error = "ceil(num_simulations / batch_size) must be <= 64";
+        return RVZ_EINVAL;
+    }
+    if (cfg->leaf_dtype != RVZ_LEAF_F32 && cfg->leaf_dtype != RVZ_LEAF_BF16) {
+        g_create_error = "leaf_dtype must be RVZ_LEAF_F32 or RVZ_LEAF_BF16";
+        return RVZ_EINVAL;
+    }
+    if (hipSetDevice(cfg->device) != hipSuccess) { g_create_error = "hipSetDevice failed"; return RVZ_EHIP; }
+    rvz_engine* e = new rvz_engine();
+    e->cfg = *cfg;
+    e->BS = bs;
+    e->NSQ = bs * bs;
+    e->NPOL = e->NSQ + 1;
+    e->E = E;
+    e->M = 1 + E * e->NSQ;
+    const int G = cfg->n_games;
+    View& v = e->v;
+    v.G = G;
+    v.M = e->M;
+    v.cpuct = (float)cfg->c_puct;
+    v.black = dalloc<uint64_t>(e, G);
+    v.white = dalloc<uint64_t>(e, G);
+    v.status = dalloc<int32_t>(e, (size_t)G * 4);
+    v.nodes = dalloc<Node>(e, (size_t)G * e->M);
+    v.meta = dalloc<uint32_t>(e, (size_t)G * e->M);
+    v.path = dalloc<int32_t>(e, (size_t)G * PATH_CAP);
+    v.pend = dalloc<int32_t>(e, G);
+    v.plen = dalloc<int32_t>(e, G);
+    v.leaf_legal = dalloc<uint64_t>(e, G);
+    v.nexp = dalloc<int32_t>(e, G);
+    float* sqrt_tab = dalloc<float>(e, (size_t)cfg->num_simulations + 1);
+    v.sqrt_tab = sqrt_tab;
+    v.rng_u = dalloc<double>(e, (size_t)G * RNG_DRAWS);
+    v.rng_pos = dalloc<int32_t>(e, G);
+    v.err = dalloc<int32_t>(e, 1);
+    for (void* p : e->allocs)
+        if (!p) { g_create_error = "hipMalloc failed (out of device memory?)"; rvz_destroy(e); return RVZ_ENOMEM; }
+    std::vector<float> tab((size_t)cfg->num_simulations + 1);
+    for (size_t n = 0; n < tab.size(); ++n) tab[n] = (float)sqrt((double)n);  // math.sqrt -> f32
+    hipError_t s = hipMemcpy(sqrt_tab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice);
+    s = s == hipSuccess ? hipMemset(v.err, 0, sizeof(int32_t)) : s;
+    s = s == hipSuccess ? hipMemset(v.pend, 0, sizeof(int32_t) * G) : s;
+    s = s == hipSuccess ? hipMemset(v.rng_pos, 0, sizeof(int32_t) * G) : s;
+    s = s == hipSuccess ? hipMemset(v.meta, 0, sizeof(uint32_t) * (size_t)G * e->M) : s;
+    if (s == hipSuccess) s = hipDeviceSynchronize();
+    if (s != hipSuccess) {
+        g_create_error = std::string("device init: ") + hipGetErrorString(s);
+        rvz_destroy(e);
+        return RVZ_EHIP;
+    }
+    *out = e;
+    // every game starts at the start position with seed = game index until rvz_env_reset
+    std::vector<uint32_t> seeds(G);
+    for (int g = 0; g < G; ++g) seeds[g] = (uint32_t)g;
+    uint32_t* dseeds = nullptr;
+    if (hipMalloc(&dseeds, sizeof(uint32_t) * G) != hipSuccess) { rvz_destroy(e); *out = nullptr; return RVZ_ENOMEM; }
+    int r = hipMemcpy(dseeds, seeds.data(), sizeof(uint32_t) * G, hipMemcpyHostToDevice) == hipSuccess
+                ? rvz_env_reset(e, dseeds, nullptr) : RVZ_EHIP;
+    if (hipDeviceSynchronize() != hipSuccess) r = RVZ_EHIP;
+    (void)hipFree(dseeds);
+    if (r != RVZ_OK) { g_create_error = e->err; rvz_destroy(e); *out = nullptr; return r; }
+    return RVZ_OK;
+}
+
+void rvz_destroy(rvz_engine* e) {
+    if (!e) return;
+    for (void* p : e->allocs)
+        if (p) (void)hipFree(p);
+    delete e;
+}
+
+int rvz_set_stream(rvz_engine* e, void* stream) {
+    if (!e) return RVZ_EINVAL;
+    e->stream = (hipStream_t)stream;
+    return RVZ_OK;
+}
+
+int rvz_sync(rvz_engine* e) {
+    if (!e) return RVZ_EINVAL;
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);
+    return RVZ_OK;
+}
+
+int rvz_check(rvz_engine* e, int32_t* host_err) {
+    if (!e) return RVZ_EINVAL;
+    int32_t h = 0;
+    RVZ_HIP(hipMemcpyAsync(&h, e->v.err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream), e);
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);
+    if (host_err) *host_err = h;
+    if (h) {
+        RVZ_HIP(hipMemsetAsync(e->v.err, 0, sizeof(int32_t), e->stream), e);
+        e->err = "device error word " + std::to_string(h) +
+                 " (1: rng stream exhausted, 2: node pool, 4: path depth)";
+        return RVZ_EDEVICE;
+    }
+    return RVZ_OK;
+}
+
+#define DISPATCH_BS(e, KERNEL8, KERNEL6) ((e)->BS == 8 ? (KERNEL8) : (KERNEL6))
+
+int rvz_env_reset(rvz_engine* e, const uint32_t* seeds, const uint8_t* mask) {
+    if (!e || !seeds) return RVZ_EINVAL;
+    dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    if (e->BS == 8) hipLaunchKernelGGL(k_reset<8>, grid, block, 0, e->stream, e->v, seeds, mask);
+    else hipLaunchKernelGGL(k_reset<6>, grid, block, 0, e->stream, e->v, seeds, mask);
+    e->searching = 0;
+    return launch_check(e, "k_reset");
+}
+
+int rvz_env_get(rvz_engine* e, uint64_t* black, uint64_t* white, int32_t* status) {
+    if (!e) return RVZ_EINVAL;
+    const size_t G = e->v.G;
+    if (black) RVZ_HIP(hipMemcpyAsync(black, e->v.black, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
+    if (white) RVZ_HIP(hipMemcpyAsync(white, e->v.white, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
+    if (status) RVZ_HIP(hipMemcpyAsync(status, e->v.status, G * 16, hipMemcpyDeviceToDevice, e->stream), e);
+    return RVZ_OK;
+}
+
+int rvz_env_set(rvz_engine* e, const uint64_t* black, const uint64_t* white, const int32_t* status) {
+    if (!e || !black || !white || !status) return RVZ_EINVAL;
+    const size_t G = e->v.G;
+    RVZ_HIP(hipMemcpyAsync(e->v.black, black, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
+    RVZ_HIP(hipMemcpyAsync(e->v.white, white, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
+    RVZ_HIP(hipMemcpyAsync(e->v.status, status, G * 16, hipMemcpyDeviceToDevice, e->stream), e);
+    e->searching = 0;
+    return RVZ_OK;
+}
+
+int rvz_board_legal(int32_t bs, int32_t n, const uint64_t* black, const uint64_t* white,
+                    const int32_t* status, uint64_t* out, void* stream) {
+    if ((bs != 8 && bs != 6) || n < 0 || (n > 0 && (!black || !white || !status || !out)))
+        return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    dim3 grid((n + 255) / 256), block(256);
+    if (bs == 8) hipLaunchKernelGGL(k_board_legal<8>, grid, block, 0, (hipStream_t)stream, n, black, white, status, out);
+    else hipLaunchKernelGGL(k_board_legal<6>, grid, block, 0, (hipStream_t)stream, n, black, white, status, out);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_board_apply(int32_t bs, int32_t n, uint64_t* black, uint64_t* white, int32_t* status,
+                    const int32_t* sq, int32_t* ok, void* stream) {
+    if ((bs != 8 && bs != 6) || n < 0 || (n > 0 && (!black || !white || !status || !sq)))
+        return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    dim3 grid((n + 255) / 256), block(256);
+    if (bs == 8) hipLaunchKernelGGL(k_board_apply<8>, grid, block, 0, (hipStream_t)stream, n, black, white, status, sq, ok);
+    else hipLaunchKernelGGL(k_board_apply<6>, grid, block, 0, (hipStream_t)stream, n, black, white, status, sq, ok);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_board_canonical(int32_t bs, int32_t n, const uint64_t* black, const uint64_t* white,
+                        const int32_t* status, float* out, void* stream) {
+    if ((bs != 8 && bs != 6) || n < 0 || (n > 0 && (!black || !white || !status || !out)))
+        return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    const int total = n * bs * bs;
+    dim3 grid((total + 255) / 256), block(256);
+    if (bs == 8) hipLaunchKernelGGL(k_board_canonical<8>, grid, block, 0, (hipStream_t)stream, n, black, white, status, out);
+    else hipLaunchKernelGGL(k_board_canonical<6>, grid, block, 0, (hipStream_t)stream, n, black, white, status, out);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_env_legal(rvz_engine* e, uint64_t* out) {
+    if (!e) return RVZ_EINVAL;
+    int r = rvz_board_legal(e->BS, e->v.G, e->v.black, e->v.white, e->v.status, out, e->stream);
+    if (r != RVZ_OK) e->err = "rvz_env_legal launch failed";
+    else e->counters[1] += 1;
+    return r;
+}
+
+int rvz_env_apply(rvz_engine* e, const int32_t* sq, int32_t* ok) {
+    if (!e) return RVZ_EINVAL;
+    int r = rvz_board_apply(e->BS, e->v.G, e->v.black, e->v.white, e->v.status, sq, ok, e->stream);
+    if (r != RVZ_OK) e->err = "rvz_env_apply launch failed";
+    else e->counters[1] += 1;
+    e->searching = 0;
+    return r;
+}
+
+int rvz_search_begin(rvz_engine* e) {
+    if (!e) return RVZ_EINVAL;
+    e->next_batch = 0;
+    e->searching = 1;
+    return RVZ_OK;
+}
+
+int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
+    if (!e || !leaf_x || !need) return RVZ_EINVAL;
+    if (!e->searching) { e->err = "rvz_search_step before rvz_search_begin"; return RVZ_EINVAL; }
+    const int S = e->cfg.num_simulations, B = e->cfg.batch_size;
+    const int start = e->next_batch * B;
+    if (start >= S) return RVZ_DONE;
+    const int bsz = S - start < B ? S - start : B;
+    const int first = e->next_batch == 0;
+    dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    if (e->cfg.leaf_dtype == RVZ_LEAF_F32) {
+        float* x = (float*)leaf_x;
+        if (e->BS == 8) hipLaunchKernelGGL((k_select<8, float>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
+        else hipLaunchKernelGGL((k_select<6, float>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
+    } else {
+        __hip_bfloat16* x = (__hip_bfloat16*)leaf_x;
+        if (e->BS == 8) hipLaunchKernelGGL((k_select<8, __hip_bfloat16>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
+        else hipLaunchKernelGGL((k_select<6, __hip_bfloat16>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
+    }
+    e->next_batch += 1;
+    e->counters[0] += 1;
+    return launch_check(e, "k_select");
+}
+
+int rvz_search_submit(rvz_engine* e, const float* policy, int32_t is_logits, const float* value) {
+    if (!e || !policy || !value) return RVZ_EINVAL;
+    dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    if (e->BS == 8) hipLaunchKernelGGL(k_expand_backup<8>, grid, block, 0, e->stream, e->v, policy, is_logits, value);
+    else hipLaunchKernelGGL(k_expand_backup<6>, grid, block, 0, e->stream, e->v, policy, is_logits, value);
+    return launch_check(e, "k_expand_backup");
+}
+
+int rvz_search_visits(rvz_engine* e, int32_t* out) {
+    if (!e || !out) return RVZ_EINVAL;
+    dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    if (e->BS == 8) hipLaunchKernelGGL(k_visits<8>, grid, block, 0, e->stream, e->v, out);
+    else hipLaunchKernelGGL(k_visits<6>, grid, block, 0, e->stream, e->v, out);
+    return launch_check(e, "k_visits");
+}
+
+int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, int32_t* out_idx,
+            double* out_p) {
+    if (!e || !out_idx || !out_p) return RVZ_EINVAL;
+    dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    if (e->BS == 8) hipLaunchKernelGGL(k_act<8>, grid, block, 0, e->stream, e->v, temperature, u, apply, out_idx, out_p);
+    else hipLaunchKernelGGL(k_act<6>, grid, block, 0, e->stream, e->v, temperature, u, apply, out_idx, out_p);
+    if (apply) e->searching = 0;
+    return launch_check(e, "k_act");
+}
+
+int rvz_counters(const rvz_engine* e, int64_t* out2) {
+    if (!e || !out2) return RVZ_EINVAL;
+    out2[0] = e->counters[0];
+    out2[1] = e->counters[1];
+    return RVZ_OK;
+}
+
+int rvz_footprint(const rvz_engine* e, int64_t* bytes_tree, int64_t* bytes_env) {
+    if (!e) return RVZ_EINVAL;
+    const int64_t G = e->v.G;
+    if (bytes_tree) *bytes_tree = G * e->M * (int64_t)(sizeof(Node) + sizeof(uint32_t)) + G * (PATH_CAP * 4 + 4 * 4 + 8);
+    if (bytes_env) *bytes_env = G * (8 + 8 + 16) + G * (RNG_DRAWS * 8 + 4);
+    return RVZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+"""ctypes binding of librvz.so (the C-ABI declared in include/rvz.h).
+
+The library is built in-tree (``make -C alphazero-reversi_amd`` or ``__graft_entry__.build()``)
+and is the ONLY implementation of the hot path: there is no CPU fallback. Loading fails loudly
+when the library is missing, and every call that returns an error code raises ``RvzError``.
+
+torch is imported first so that librvz.so binds to the HIP runtime torch already loaded (both
+carry the soname libamdhip64.so.7): torch streams and tensors are then valid in our launches.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librvz.so")
+
+RVZ_OK, RVZ_DONE = 0, 1
+RVZ_LEAF_F32, RVZ_LEAF_BF16 = 0, 1
+
+
+class RvzError(RuntimeError):
+    pass
+
+
+class Config(C.Structure):
+    _fields_ = [("board_size", C.c_int32), ("n_games", C.c_int32),
+                ("num_simulations", C.c_int32), ("batch_size", C.c_int32),
+                ("c_puct", C.c_double), ("device", C.c_int32), ("leaf_dtype", C.c_int32)]
+
+
+# name -> (restype, argtypes); kept in the order of include/rvz.h
+_P = C.c_void_p
+SIGNATURES = {
+    "rvz_version": (C.c_int, []),
+    "rvz_create": (C.c_int, [C.POINTER(Config), C.POINTER(_P)]),
+    "rvz_destroy": (None, [_P]),
+    "rvz_last_error": (C.c_char_p, [_P]),
+    "rvz_set_stream": (C.c_int, [_P, _P]),
+    "rvz_sync": (C.c_int, [_P]),
+    "rvz_check": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "rvz_env_reset": (C.c_int, [_P, _P, _P]),
+    "rvz_env_get": (C.c_int, [_P, _P, _P, _P]),
+    "rvz_env_set": (C.c_int, [_P, _P, _P, _P]),
+    "rvz_env_legal": (C.c_int, [_P, _P]),
+    "rvz_env_apply": (C.c_int, [_P, _P, _P]),
+    "rvz_board_legal": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
+    "rvz_board_apply": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
+    "rvz_board_canonical": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
+    "rvz_search_begin": (C.c_int, [_P]),
+    "rvz_search_step": (C.c_int, [_P, _P, _P]),
+    "rvz_search_submit": (C.c_int, [_P, _P, C.c_int32, _P]),
+    "rvz_search_visits": (C.c_int, [_P, _P]),
+    "rvz_act": (C.c_int, [_P, C.c_double, _P, C.c_int32, _P, _P]),
+    "rvz_counters": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "rvz_footprint": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load librvz.so (no GPU needed to load; calls that launch kernels need one)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RvzError(f"{LIB_PATH} is missing: build it with `make -C alphazero-reversi_amd` "
+                           "(there is no CPU fallback for the rvz hot path)")
+        lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, handle=None, what: str = "") -> int:
+    if rc < 0:
+        msg = load().rvz_last_error(handle)
+        raise RvzError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+def ptr(t) -> int:
+    """Device pointer of a contiguous CUDA (HIP) tensor; 16-byte aligned as the kernels assume."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RvzError("rvz buffers must be device tensors (no host fallback)")
+    if not t.is_contiguous():
+        raise RvzError("rvz buffers must be contiguous")
+    p = t.data_ptr()
+    if p % 16:
+        raise RvzError("rvz buffers must be 16-byte aligned")
+    return p
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,232 @@
+"""Host mirror of the rvz engine: owns one C-ABI engine (include/rvz.h) and its device buffers.
+
+One ``Engine`` = ``n_games`` Reversi games resident in HBM, each with its own MCTS tree.
+It is what the reference's per-game ``ReversiGame`` + ``MCTS`` pair becomes when all games of a
+self-play batch are advanced in lockstep (self_play.py:80-101, mcts.py:322-694):
+
+    eng.reset(seeds)                      # ReversiGame() x n + np.random.seed per game
+    eng.search(evaluator)                 # MCTS.search for every live game
+    idx, p = eng.act(temperature)         # get_action_probs tail + game.make_move
+
+Every tensor handed to the library is a device tensor on ``eng.device``; all work is enqueued on
+the current torch stream of that device (graph-capturable: no host syncs inside ``search``/``act``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Optional, Sequence, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import RVZ_DONE, RVZ_LEAF_BF16, RVZ_LEAF_F32, RvzError, check, ptr
+
+U64 = 0xFFFFFFFFFFFFFFFF
+
+
+def to_signed64(x: int) -> int:
+    x &= U64
+    return x - (1 << 64) if x >> 63 else x
+
+
+def to_unsigned64(x: int) -> int:
+    return int(x) & U64
+
+
+class Engine:
+    def __init__(self, n_games: int, num_simulations: int = 800, batch_size: int = 64,
+                 c_puct: float = 1.0, board_size: int = 8, device=None,
+                 leaf_dtype: torch.dtype = torch.float32):
+        if not torch.cuda.is_available():
+            raise RvzError("rvz needs a HIP device (MI355X); there is no CPU fallback")
+        self.lib = _lib.load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.n_games, self.board_size = int(n_games), int(board_size)
+        self.num_simulations, self.batch_size = int(num_simulations), int(batch_size)
+        self.c_puct = float(c_puct)
+        self.nsq = board_size * board_size
+        self.npol = self.nsq + 1
+        if leaf_dtype not in (torch.float32, torch.bfloat16):
+            raise RvzError("leaf_dtype must be torch.float32 or torch.bfloat16")
+        self.leaf_dtype = leaf_dtype
+        cfg = _lib.Config(board_size, n_games, num_simulations, batch_size, c_puct,
+                          self.device.index,
+                          RVZ_LEAF_F32 if leaf_dtype == torch.float32 else RVZ_LEAF_BF16)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            check(self.lib.rvz_create(C.byref(cfg), C.byref(h)), None, "rvz_create")
+        self._h = h
+        G, dev = self.n_games, self.device
+        self.leaf_x = torch.zeros(G, 3, board_size, board_size, dtype=leaf_dtype, device=dev)
+        self.need = torch.zeros(G, dtype=torch.int32, device=dev)
+        self.visits_buf = torch.zeros(G, self.npol, dtype=torch.int32, device=dev)
+        self.p_buf = torch.zeros(G, self.npol, dtype=torch.float64, device=dev)
+        self.idx_buf = torch.zeros(G, dtype=torch.int32, device=dev)
+        self.black = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.white = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.status = torch.zeros(G, 4, dtype=torch.int32, device=dev)
+        self.n_batches = -(-num_simulations // batch_size)
+
+    # ------------------------------------------------------------------ plumbing
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass
+            self.lib.rvz_destroy(h)
+            self._h = None
+
+    def _stream(self):
+        s = _lib.stream_handle(self.device)
+        check(self.lib.rvz_set_stream(self._h, s), self._h, "rvz_set_stream")
+
+    def _call(self, name: str, *args) -> int:
+        return check(getattr(self.lib, name)(self._h, *args), self._h, name)
+
+    def check(self) -> None:
+        """Synchronise and raise if a kernel set the device error word."""
+        self._stream()
+        err = C.c_int32(0)
+        self._call("rvz_check", C.byref(err))
+
+    def counters(self) -> Tuple[int, int]:
+        out = (C.c_int64 * 2)()
+        self.lib.rvz_counters(self._h, out)
+        return int(out[0]), int(out[1])
+
+    def footprint(self) -> Tuple[int, int]:
+        a, b = C.c_int64(), C.c_int64()
+        self.lib.rvz_footprint(self._h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    # ------------------------------------------------------------------ env
+    def reset(self, seeds: Optional[Sequence[int]] = None, mask: Optional[torch.Tensor] = None):
+        """ReversiGame() for every (masked) game + np.random.seed(seeds[g]) per game."""
+        self._stream()
+        if seeds is None:
+            seeds = range(self.n_games)
+        if not isinstance(seeds, torch.Tensor):
+            seeds = torch.tensor([int(s) & 0xFFFFFFFF for s in seeds], dtype=torch.int64)
+        s = seeds.to(self.device).to(torch.int64).bitwise_and(0xFFFFFFFF).to(torch.int32)
+        if s.numel() != self.n_games:
+            raise RvzError("one seed per game")
+        m = None if mask is None else mask.to(self.device, torch.uint8).contiguous()
+        self._seeds = s.contiguous()
+        self._call("rvz_env_reset", ptr(self._seeds), ptr(m) if m is not None else None)
+
+    def get_state(self):
+        """(black int64[G], white int64[G], status int32[G,4]) device tensors (bit patterns)."""
+        self._stream()
+        self._call("rvz_env_get", ptr(self.black), ptr(self.white), ptr(self.status))
+        return self.black, self.white, self.status
+
+    def set_state(self, black: torch.Tensor, white: torch.Tensor, status: torch.Tensor):
+        self._stream()
+        b = black.to(self.device, torch.int64).contiguous()
+        w = white.to(self.device, torch.int64).contiguous()
+        st = status.to(self.device, torch.int32).contiguous()
+        self._call("rvz_env_set", ptr(b), ptr(w), ptr(st))
+        torch.cuda.current_stream(self.device).synchronize()  # b, w, st are temporaries
+
+    def legal(self) -> torch.Tensor:
+        self._stream()
+        out = torch.empty(self.n_games, dtype=torch.int64, device=self.device)
+        self._call("rvz_env_legal", ptr(out))
+        return out
+
+    def apply(self, sq: torch.Tensor) -> torch.Tensor:
+        self._stream()
+        s = sq.to(self.device, torch.int32).contiguous()
+        ok = torch.empty(self.n_games, dtype=torch.int32, device=self.device)
+        self._call("rvz_env_apply", ptr(s), ptr(ok))
+        return ok
+
+    # ------------------------------------------------------------------ search
+    def search_begin(self):
+        self._call("rvz_search_begin")
+
+    def search_step(self) -> bool:
+        """One batch up to the NN call. False once every batch of this search was issued."""
+        self._stream()
+        rc = self._call("rvz_search_step", ptr(self.leaf_x), ptr(self.need))
+        return rc != RVZ_DONE
+
+    def search_submit(self, policy: torch.Tensor, value: torch.Tensor, is_logits: bool):
+        if policy.dtype != torch.float32 or value.dtype != torch.float32:
+            raise RvzError("policy/value must be float32")
+        if policy.shape != (self.n_games, self.npol) or value.shape != (self.n_games,):
+            raise RvzError(f"policy must be [{self.n_games},{self.npol}], value [{self.n_games}]")
+        self._stream()
+        self._call("rvz_search_submit", ptr(policy), int(bool(is_logits)), ptr(value))
+
+    def search(self, evaluator: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],
+               fused_softmax: bool = True):
+        """MCTS.search for every live game. evaluator(leaf_x) -> (logits, value).
+
+        fused_softmax=False applies torch's F.softmax (the reference's mcts.py:596) before the
+        expand kernel instead of the kernel's fused softmax."""
+        self.search_begin()
+        while self.search_step():
+            logits, value = evaluator(self.leaf_x)
+            logits = logits.float().contiguous()
+            value = value.float().contiguous()
+            if fused_softmax:
+                self.search_submit(logits, value, True)
+            else:
+                self.search_submit(torch.softmax(logits, dim=1).contiguous(), value, False)
+
+    def visits(self) -> torch.Tensor:
+        self._stream()
+        self._call("rvz_search_visits", ptr(self.visits_buf))
+        return self.visits_buf
+
+    def act(self, temperature: float = 1.0, u: Optional[torch.Tensor] = None,
+            apply: bool = True):
+        """get_action_probs tail (+ make_move): returns (idx int32[G], p float64[G,npol])."""
+        self._stream()
+        uu = None
+        if u is not None:
+            uu = u.to(self.device, torch.float64).contiguous()
+            self._u_keep = uu
+        self._call("rvz_act", float(temperature), ptr(uu) if uu is not None else None,
+                   int(bool(apply)), ptr(self.idx_buf), ptr(self.p_buf))
+        return self.idx_buf, self.p_buf
+
+
+# -------------------------------------------------------------------------- board kernels
+def board_legal(black: torch.Tensor, white: torch.Tensor, status: torch.Tensor,
+                board_size: int = 8) -> torch.Tensor:
+    lib = _lib.load()
+    n = black.numel()
+    out = torch.empty(n, dtype=torch.int64, device=black.device)
+    check(lib.rvz_board_legal(board_size, n, ptr(black), ptr(white), ptr(status), ptr(out),
+                              _lib.stream_handle(black.device)), None, "rvz_board_legal")
+    return out
+
+
+def board_apply(black: torch.Tensor, white: torch.Tensor, status: torch.Tensor, sq: torch.Tensor,
+                board_size: int = 8) -> torch.Tensor:
+    """In place on (black, white, status); returns make_move's bool per board."""
+    lib = _lib.load()
+    n = black.numel()
+    ok = torch.empty(n, dtype=torch.int32, device=black.device)
+    check(lib.rvz_board_apply(board_size, n, ptr(black), ptr(white), ptr(status),
+                              ptr(sq.to(torch.int32).contiguous()), ptr(ok),
+                              _lib.stream_handle(black.device)), None, "rvz_board_apply")
+    return ok
+
+
+def board_canonical(black: torch.Tensor, white: torch.Tensor, status: torch.Tensor,
+                    board_size: int = 8) -> torch.Tensor:
+    lib = _lib.load()
+    n = black.numel()
+    out = torch.empty(n, 3, board_size, board_size, dtype=torch.float32, device=black.device)
+    check(lib.rvz_board_canonical(board_size, n, ptr(black), ptr(white), ptr(status), ptr(out),
+                                  _lib.stream_handle(black.device)), None, "rvz_board_canonical")
+    return out

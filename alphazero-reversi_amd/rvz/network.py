@@ -1,0 +1,166 @@
+"""The policy/value ResNet at the leaf-evaluation boundary.
+
+``AlphaZeroNetwork`` is state_dict-compatible with the reference's
+src/model/network.py:30-117 (same module names and shapes, same forward graph), so reference
+checkpoints load into it; ``load_reference_state_dict`` drops the duplicated
+``_script_module.*`` keys that the reference's TorchScript compile registers
+(pipeline.py:410-418). It is the model protocol of the reference (``predict(x) -> (logits[B,65],
+value[B])``, network.py:136-158) and stays plain PyTorch-ROCm: the leaf evaluator is the
+boundary callee, not part of the rvz hot path.
+
+``LeafEvaluator`` is the inference form used by the self-play driver: eval-mode BatchNorm folded
+into the preceding convolution, NHWC (channels_last) activations for MIOpen, fp32 (the reference's
+precision) or bf16, and fixed-shape calls so the whole ply can be captured in one HIP graph.
+"""
+from __future__ import annotations
+
+from typing import Dict, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class _Residual(nn.Module):
+    """conv-bn-relu-conv-bn + skip, relu (network.py:14-28)."""
+
+    def __init__(self, width: int):
+        super().__init__()
+        self.conv1 = nn.Conv2d(width, width, 3, padding=1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, padding=1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+
+    def forward(self, x):
+        y = F.relu(self.bn1(self.conv1(x)))
+        return F.relu(self.bn2(self.conv2(y)) + x)
+
+
+class AlphaZeroNetwork(nn.Module):
+    """3 -> F stem, N residual blocks, 2-plane policy head (S*S+1 logits), 1-plane value head."""
+
+    def __init__(self, board_size: int = 8, num_res_blocks: int = 5, num_filters: int = 128):
+        super().__init__()
+        self.board_size = board_size
+        self.num_filters = num_filters
+        cells = board_size * board_size
+        self.conv = nn.Conv2d(3, num_filters, 3, padding=1, bias=False)
+        self.bn = nn.BatchNorm2d(num_filters)
+        self.res_blocks = nn.ModuleList(_Residual(num_filters) for _ in range(num_res_blocks))
+        self.policy_conv = nn.Conv2d(num_filters, 2, 1, bias=False)
+        self.policy_bn = nn.BatchNorm2d(2)
+        self.policy_fc = nn.Linear(2 * cells, cells + 1)
+        self.value_conv = nn.Conv2d(num_filters, 1, 1, bias=False)
+        self.value_bn = nn.BatchNorm2d(1)
+        self.value_fc1 = nn.Linear(cells, 256)
+        self.value_fc2 = nn.Linear(256, 1)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        """Kaiming-normal fan-out for conv/linear weights, BN affine = (1, 0) (network.py:71-78)."""
+        for m in self.modules():
+            if isinstance(m, (nn.Conv2d, nn.Linear)):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def trunk(self, x):
+        x = F.relu(self.bn(self.conv(x)))
+        for blk in self.res_blocks:
+            x = blk(x)
+        return x
+
+    def forward(self, x) -> Tuple[torch.Tensor, torch.Tensor]:
+        h = self.trunk(x)
+        n = h.shape[0]
+        pol = F.relu(self.policy_bn(self.policy_conv(h))).reshape(n, -1)
+        val = F.relu(self.value_bn(self.value_conv(h))).reshape(n, -1)
+        val = torch.tanh(self.value_fc2(F.relu(self.value_fc1(val))))
+        return self.policy_fc(pol), val.squeeze(1)
+
+    def predict(self, board_state, valid_moves=None):
+        """network.py:136-158: adds the batch dim for a single [3,S,S] state."""
+        if board_state.dim() == 3:
+            board_state = board_state.unsqueeze(0)
+        return self.forward(board_state)
+
+
+def load_reference_state_dict(net: nn.Module, sd: Dict[str, torch.Tensor]) -> None:
+    """Load a reference checkpoint; tolerates the TorchScript `_script_module.` duplicates."""
+    plain = {k: v for k, v in sd.items() if not k.startswith("_script_module.")}
+    if not plain:  # only the scripted copy was saved
+        plain = {k[len("_script_module."):]: v for k, v in sd.items()}
+    net.load_state_dict(plain)
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+    w = conv.weight * scale.reshape(-1, 1, 1, 1)
+    b = bn.bias - bn.running_mean * scale
+    return w.detach(), b.detach()
+
+
+class LeafEvaluator:
+    """Inference-only evaluator over a fixed leaf batch: (logits f32 [n,S*S+1], value f32 [n]).
+
+    BN is folded (eval mode), activations are channels_last, compute dtype is ``dtype``
+    (torch.float32 = the reference's precision, or torch.bfloat16); outputs are float32 so the
+    rvz expand kernel reads them directly (it fuses the softmax).
+    """
+
+    def __init__(self, net: AlphaZeroNetwork, dtype=torch.float32, device=None):
+        net = net.eval()
+        dev = torch.device(device) if device is not None else next(net.parameters()).device
+        self.dtype, self.device = dtype, dev
+        self.board_size = net.board_size
+        cl = torch.channels_last
+
+        def conv_param(conv, bn):
+            w, b = _fold(conv, bn)
+            return (w.to(dev, dtype).contiguous(memory_format=cl), b.to(dev, dtype))
+
+        with torch.no_grad():
+            self.stem = conv_param(net.conv, net.bn)
+            self.blocks = [(conv_param(b.conv1, b.bn1), conv_param(b.conv2, b.bn2))
+                           for b in net.res_blocks]
+            self.pconv = conv_param(net.policy_conv, net.policy_bn)
+            self.vconv = conv_param(net.value_conv, net.value_bn)
+            # NCHW flatten order of the heads: permute the FC input columns once instead of
+            # converting the activation back to NCHW
+            cells = self.board_size ** 2
+
+            def fc_nhwc(fc, planes):
+                w = fc.weight.detach().reshape(fc.out_features, planes, cells)
+                w = w.permute(0, 2, 1).reshape(fc.out_features, planes * cells)
+                return w.to(dev, dtype).contiguous(), fc.bias.detach().to(dev, dtype)
+
+            self.pfc = fc_nhwc(net.policy_fc, 2)
+            self.vfc1 = fc_nhwc(net.value_fc1, 1)
+            self.vfc2 = (net.value_fc2.weight.detach().to(dev, dtype),
+                         net.value_fc2.bias.detach().to(dev, dtype))
+
+    @torch.no_grad()
+    def __call__(self, x: torch.Tensor):
+        cl = torch.channels_last
+        h = x.to(self.dtype).contiguous(memory_format=cl)
+        w, b = self.stem
+        h = F.relu(F.conv2d(h, w, b, padding=1))
+        for (w1, b1), (w2, b2) in self.blocks:
+            y = F.relu(F.conv2d(h, w1, b1, padding=1))
+            h = F.relu(F.conv2d(y, w2, b2, padding=1) + h)
+        n = h.shape[0]
+        p = F.relu(F.conv2d(h, *self.pconv))          # [n,2,S,S] channels_last == NHWC memory
+        p = p.permute(0, 2, 3, 1).reshape(n, -1)
+        logits = F.linear(p, *self.pfc)
+        v = F.relu(F.conv2d(h, *self.vconv)).reshape(n, -1)
+        v = torch.tanh(F.linear(F.relu(F.linear(v, *self.vfc1)), *self.vfc2)).squeeze(1)
+        return logits.float(), v.float()
+
+    def flops_per_row(self) -> int:
+        """Multiply-adds x2 of one leaf evaluation (convs + FCs)."""
+        cells = self.board_size ** 2
+        f = self.stem[0].shape[0]
+        macs = cells * f * 3 * 9 + len(self.blocks) * 2 * cells * f * f * 9
+        macs += cells * f * 3 + 2 * cells * (cells + 1) + cells * 256 + 256
+        return 2 * macs

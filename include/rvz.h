@@ -1,0 +1,116 @@
+/*
+ * rvz.h — C-ABI of the MI355X-native Reversi self-play engine (librvz.so, gfx950).
+ *
+ * The reference (RandomMike1280/AlphaZero-Reversi) has no FFI on this path: its boundary is three
+ * duck-typed Python protocols (game / model / MCTS). Each entry point below replaces one piece of
+ * that surface; the line each one replaces is cited next to it. The Python host mirror in
+ * alphazero-reversi_amd/rvz (ReversiGame, MCTS, SelfPlay) binds these with ctypes
+ * (INTEGRATION.md shows the binding a reference maintainer would add).
+ *
+ * Conventions
+ *  - Every array argument is a DEVICE pointer (HBM, e.g. torch.Tensor.data_ptr()) unless the
+ *    comment says "host". Work is enqueued on the engine's stream (rvz_set_stream) or on the
+ *    stream argument; nothing here synchronises except rvz_sync / rvz_check.
+ *  - Squares are row-major: square s <-> (row, col) = (s / S, s % S), bit s of a bitboard
+ *    (board.py:49). The policy index S*S is the pass move (-1, -1) (mcts.py:666-667,687-688).
+ *  - Game status is int32[4] per game: {side to move 1|2, game_over 0|1, winner -1 (None)|0|1|2,
+ *    passed_moves_in_a_row} (board.py:33-37, game.py:20-23).
+ *  - Return codes: RVZ_OK (0) or a negative RVZ_E*; rvz_last_error() explains the last failure.
+ *    Game-level illegality is data, not an error: make_move's False is written to out_ok.
+ *  - One engine per device per process; not re-entrant. The caller owns every in/out buffer.
+ */
+#ifndef RVZ_H
+#define RVZ_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RVZ_OK 0
+#define RVZ_DONE 1          /* rvz_search_step: every batch of this search has been issued */
+#define RVZ_EINVAL (-22)
+#define RVZ_ENOMEM (-12)
+#define RVZ_EHIP (-5)
+#define RVZ_EDEVICE (-71)   /* a kernel raised its device-side error word (rvz_check) */
+
+#define RVZ_LEAF_F32 0      /* leaf planes in float32, exactly game.get_canonical_state() */
+#define RVZ_LEAF_BF16 1     /* the same 0/1 planes as bfloat16 (exact) for a bf16 evaluator */
+
+typedef struct rvz_engine rvz_engine;
+
+typedef struct rvz_config {
+    int32_t board_size;       /* 8 (reference; board.py:27-28) or 6 (build-defined variant) */
+    int32_t n_games;          /* games owned by this engine (one tree each) */
+    int32_t num_simulations;  /* MCTS(num_simulations=800)  mcts.py:197 */
+    int32_t batch_size;       /* MCTS(batch_size=64)        mcts.py:198; ceil(sims/batch) <= 64 */
+    double c_puct;            /* MCTS(c_puct=1.0)           mcts.py:197 */
+    int32_t device;           /* HIP device ordinal */
+    int32_t leaf_dtype;       /* RVZ_LEAF_F32 | RVZ_LEAF_BF16 */
+} rvz_config;
+
+/* ---- lifetime -------------------------------------------------------------------------- */
+/* replaces MCTS.__init__ (mcts.py:197-235) + the per-game ReversiGame() of self_play.py:71 */
+int rvz_create(const rvz_config *cfg /* host */, rvz_engine **out /* host */);
+void rvz_destroy(rvz_engine *e);
+const char *rvz_last_error(const rvz_engine *e);          /* e may be NULL: last create error */
+int rvz_set_stream(rvz_engine *e, void *hip_stream);        /* hipStream_t; NULL = default */
+int rvz_sync(rvz_engine *e);                                /* hipStreamSynchronize */
+int rvz_check(rvz_engine *e, int32_t *host_err);            /* sync + read/clear device error */
+int rvz_version(void);
+
+/* ---- env, engine-owned (board.py / game.py over n_games boards in HBM) --------------------- */
+/* Reset games to the start position (board.py:25-39) and seed each game's numpy-compatible
+ * MT19937 stream with seeds[g] (np.random.seed, the RNG behind mcts.py:684). mask: reset only
+ * games with mask[g] != 0 (NULL = all). */
+int rvz_env_reset(rvz_engine *e, const uint32_t *seeds, const uint8_t *mask);
+int rvz_env_get(rvz_engine *e, uint64_t *black, uint64_t *white, int32_t *status);
+int rvz_env_set(rvz_engine *e, const uint64_t *black, const uint64_t *white, const int32_t *status);
+/* ReversiGame.get_valid_moves (game.py:72-79 -> board.py:70-133) as a bitmask per game */
+int rvz_env_legal(rvz_engine *e, uint64_t *out_mask);
+/* ReversiGame.make_move (game.py:36-70 -> board.py:135-251); sq[g] = -1 is the pass (-1,-1) */
+int rvz_env_apply(rvz_engine *e, const int32_t *sq, int32_t *out_ok);
+
+/* ---- board kernels on caller arrays (stateless; n boards) ------------------------------ */
+int rvz_board_legal(int32_t board_size, int32_t n, const uint64_t *black, const uint64_t *white,
+                    const int32_t *status, uint64_t *out_mask, void *hip_stream);
+int rvz_board_apply(int32_t board_size, int32_t n, uint64_t *black, uint64_t *white,
+                    int32_t *status, const int32_t *sq, int32_t *out_ok, void *hip_stream);
+/* ReversiGame.get_canonical_state (game.py:131-162): float32 [n, 3, S, S] */
+int rvz_board_canonical(int32_t board_size, int32_t n, const uint64_t *black,
+                        const uint64_t *white, const int32_t *status, float *out,
+                        void *hip_stream);
+
+/* ---- search (MCTS.search, mcts.py:322-407, one tree per game, lockstep over games) -------- */
+/* New root per live game from the engine's env state (mcts.py:334-341). */
+int rvz_search_begin(rvz_engine *e);
+/* Issue the next batch (mcts.py:348-392 up to the NN call): traversals, immediate terminal
+ * backups, _process_batch pass 1. Writes the leaf planes of game g into row g of leaf_x
+ * ([n_games, 3, S, S], leaf_dtype) and need[g] = the number of queued traversal copies that
+ * wait for row g (0: row g unused this batch). Returns RVZ_DONE (and does nothing) when the
+ * search has issued all ceil(num_simulations / batch_size) batches. */
+int rvz_search_step(rvz_engine *e, void *leaf_x, int32_t *need);
+/* _process_batch pass 2 (mcts.py:600-623): expand every waiting leaf from policy row g and back
+ * up value[g]. policy is [n_games, S*S+1] float32: softmaxed probabilities (is_logits = 0,
+ * exactly mcts.py:596's input) or raw logits (is_logits = 1: softmax fused into the kernel). */
+int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, const float *value);
+/* {move: child.visit_count} (mcts.py:406-407) as int32 [n_games, S*S+1] */
+int rvz_search_visits(rvz_engine *e, int32_t *out);
+/* get_action_probs' tail (mcts.py:656-692) + SelfPlay's make_move (self_play.py:98):
+ * p (float64 [n_games, S*S+1]) and the chosen index (int32 [n_games]; S*S = pass, -2 = game
+ * already over) per game. Samples with each game's MT19937 stream, or with u[g] when u != NULL
+ * (float64 [n_games]; the value np.random.random_sample() would return). apply != 0 then plays
+ * the move on the engine's env (ReversiGame.make_move semantics). */
+int rvz_act(rvz_engine *e, double temperature, const double *u, int32_t apply, int32_t *out_idx,
+            double *out_p);
+
+/* ---- introspection (tests / bench) -------------------------------------------------------- */
+/* Host copy of per-engine counters: [0] search batches issued, [1] kernel launches. */
+int rvz_counters(const rvz_engine *e, int64_t *out2 /* host */);
+/* Sizes of the engine's device-resident state, for DESIGN/bench accounting (host out). */
+int rvz_footprint(const rvz_engine *e, int64_t *bytes_tree, int64_t *bytes_env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RVZ_H */
