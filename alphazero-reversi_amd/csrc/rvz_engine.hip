@@ -85,6 +85,7 @@ struct View {  // kernel argument: device pointers + sizes
     double* rng_u;          // [G][RNG_DRAWS]
     int32_t* rng_pos;
     int32_t* err;
+    unsigned long long* stats;  // [4] algorithmic bytes: select, expand_backup, act, launches; or null
 };
 
 enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4 };
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
         root_meta = meta[0];
     }
     int copies = 0, plen = 0, mypath = 0;
+    unsigned long long ab = 32 + (first ? 20 : 4);  // game state read; root node/meta
     if (!root.over) {
         int remaining = bsz;
         for (;;) {
@@ -216,6 +218,11 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
                     }
                 }
                 const int ci = wave_argmax_first(score, lane < nch, lane);
+                if (v.stats) {  // parent N, the children's nodes, the chosen child's meta, cache writes
+                    const int nw = __popcll(__ballot(lane < nch && score == score &&
+                                                     !isinf(score)));
+                    ab += 4 + 16ull * nch + 4 + 4ull * nw;
+                }
                 node = base + ci;
                 m = meta[node];
                 make_move<BS>(sim, m_sq(m));
@@ -229,6 +236,7 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
             }
             if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
                 backup_path(nodes, mypath, depth + 1, m_tv(m), 1, lane);
+                ab += 32ull * (depth + 1);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 if (--remaining == 0) break;
                 continue;
@@ -241,6 +249,7 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
                 if (lane == 0) meta[node] = m | (1u << 8) | (code << 9);
                 backup_path(nodes, mypath, depth + 1, w == 1 ? 1.0f : (w == 2 ? -1.0f : 0.0f),
                             remaining, lane);
+                ab += 4 + 32ull * (depth + 1);
                 break;
             }
             // queue `remaining` identical copies for the NN: encode get_canonical_state() planes
@@ -255,6 +264,7 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
             }
             if (lane < plen) v.path[g * PATH_CAP + lane] = mypath;
             if (lane == 0) v.leaf_legal[g] = V;
+            ab += 3ull * NSQ * sizeof(XT) + 4ull * plen + 8;
             break;
         }
     }
@@ -262,6 +272,7 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
         need[g] = copies;
         v.pend[g] = copies;
         v.plen[g] = plen;
+        if (v.stats) atomicAdd(&v.stats[0], ab + 12);
     }
 }
 
@@ -311,6 +322,12 @@ __global__ __launch_bounds__(256) void k_expand_backup(View v, const float* __re
         v.pend[g] = 0;
     }
     backup_path(nodes, mypath, plen, value[g], copies, lane);
+    if (v.stats && lane == 0) {
+        // pend/plen/path/legal/nexp reads, policy row + value, leaf meta r/w, children, backup
+        const unsigned long long nch = (unsigned long long)__popcll(V);
+        atomicAdd(&v.stats[1], 8ull + 4ull * plen + 8 + 8 + 4ull * NPOL + 4 + 8 + 20ull * nch +
+                                   32ull * plen + 4);
+    }
 }
 
 // Dense visit count of square `lane` at the root: the root's children are the set bits of the
@@ -439,6 +456,9 @@ __global__ __launch_bounds__(256) void k_act(View v, double temperature, const d
         make_move<BS>(gm, idx == NSQ ? -1 : idx);  // (row, col) = (-1, -1) for the pass index
         if (lane == 0) store_game(v, g, gm);
     }
+    if (v.stats && lane == 0)  // state r/(w), root meta + children N, p row + idx, rng
+        atomicAdd(&v.stats[2], 32ull + (apply ? 32 : 0) + 4 + 4ull * m_nchild(v.meta[(size_t)g * v.M]) +
+                                   8ull * NPOL + 4 + 16);
 }
 
 // reset: new game (board.py:25-39) + np.random.seed(seed) random_sample() stream.
@@ -545,6 +565,7 @@ struct rvz_engine {
     int searching = 0;
     int64_t counters[2] = {0, 0};
     View v;
+    unsigned long long* stats_buf = nullptr;
     std::vector<void*> allocs;
     std::string err;
 };
@@ -634,6 +655,8 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     v.rng_u = dalloc<double>(e, (size_t)G * RNG_DRAWS);
     v.rng_pos = dalloc<int32_t>(e, G);
     v.err = dalloc<int32_t>(e, 1);
+    e->stats_buf = dalloc<unsigned long long>(e, 4);
+    v.stats = nullptr;
     for (void* p : e->allocs)
         if (!p) { g_create_error = "hipMalloc failed (out of device memory?)"; rvz_destroy(e); return RVZ_ENOMEM; }
     std::vector<float> tab((size_t)cfg->num_simulations + 1);
@@ -838,6 +861,32 @@ int rvz_counters(const rvz_engine* e, int64_t* out2) {
     if (!e || !out2) return RVZ_EINVAL;
     out2[0] = e->counters[0];
     out2[1] = e->counters[1];
+    return RVZ_OK;
+}
+
+int rvz_stats_enable(rvz_engine* e, int32_t on) {
+    if (!e) return RVZ_EINVAL;
+    e->v.stats = on ? e->stats_buf : nullptr;
+    if (on) RVZ_HIP(hipMemsetAsync(e->stats_buf, 0, 4 * sizeof(unsigned long long), e->stream), e);
+    return RVZ_OK;
+}
+
+int rvz_stats_read(rvz_engine* e, int64_t* out3) {
+    if (!e || !out3) return RVZ_EINVAL;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    RVZ_HIP(hipMemcpyAsync(h, e->stats_buf, sizeof(h), hipMemcpyDeviceToHost, e->stream), e);
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);
+    for (int i = 0; i < 3; ++i) out3[i] = (int64_t)h[i];
+    return RVZ_OK;
+}
+
+int rvz_tree_nodes(const rvz_engine* e) { return e ? e->M : RVZ_EINVAL; }
+
+int rvz_tree_export(rvz_engine* e, void* nodes_out, uint32_t* meta_out) {
+    if (!e) return RVZ_EINVAL;
+    const size_t n = (size_t)e->v.G * e->M;
+    if (nodes_out) RVZ_HIP(hipMemcpyAsync(nodes_out, e->v.nodes, n * sizeof(Node), hipMemcpyDeviceToDevice, e->stream), e);
+    if (meta_out) RVZ_HIP(hipMemcpyAsync(meta_out, e->v.meta, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream), e);
     return RVZ_OK;
 }
 

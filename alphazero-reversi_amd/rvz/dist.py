@@ -1,0 +1,78 @@
+"""Multi-GPU sharding of self-play: one process per GPU, games partitioned by rank.
+
+Self-play shards embarrassingly: every game, tree and RNG stream is independent, so
+rank r owns games [r*N/W, (r+1)*N/W) of the global game index space and runs its own engine on
+its own device with no data-path collective. The only cross-rank traffic is the benchmark's
+timing reduction (MAX over ranks) and the final sum of committed plies. The reference has no
+counterpart (mcts.py:220-226,446-542 only chunks one batch over local replicas sequentially).
+"""
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank_world() -> Tuple[int, int, int]:
+    """(rank, local_rank, world_size) from torchrun's environment (1 process when unset)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def shard_range(n_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous, balanced [start, stop) of the global game index space owned by `rank`."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    base, rem = divmod(n_total, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def shard_seeds(seed_base: int, n_total: int, rank: int, world: int) -> torch.Tensor:
+    """Per-game seeds of this rank's shard: global game g is always seeded seed_base + g."""
+    a, b = shard_range(n_total, rank, world)
+    return torch.arange(a, b, dtype=torch.int64) + seed_base
+
+
+def init(backend: str = None) -> bool:
+    """Initialise the default process group when launched by torchrun; False when single-rank."""
+    _, _, world = env_rank_world()
+    if world <= 1 or dist.is_initialized():
+        return dist.is_initialized()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"   # nccl == RCCL on ROCm
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group(backend=backend)
+    return True
+
+
+def _device_for_backend():
+    if dist.is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def reduce_max(x: float) -> float:
+    if not dist.is_initialized():
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_device_for_backend())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def reduce_sum(x: float) -> float:
+    if not dist.is_initialized():
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=_device_for_backend())
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def barrier():
+    if dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()

@@ -105,6 +105,26 @@ class Engine:
         self.lib.rvz_footprint(self._h, C.byref(a), C.byref(b))
         return a.value, b.value
 
+    def stats_enable(self, on: bool = True):
+        self._stream()
+        self._call("rvz_stats_enable", int(bool(on)))
+
+    def stats_read(self):
+        """Algorithmic bytes moved since stats_enable: (select, expand_backup, act)."""
+        self._stream()
+        out = (C.c_int64 * 3)()
+        self._call("rvz_stats_read", out)
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def tree(self):
+        """(nodes int32[G, M, 4] = {N, W, P, C} (W/P/C as float32 bits), meta uint32-as-int32[G, M])."""
+        self._stream()
+        M = self.lib.rvz_tree_nodes(self._h)
+        nodes = torch.empty(self.n_games, M, 4, dtype=torch.int32, device=self.device)
+        meta = torch.empty(self.n_games, M, dtype=torch.int32, device=self.device)
+        self._call("rvz_tree_export", ptr(nodes), ptr(meta))
+        return nodes, meta
+
     # ------------------------------------------------------------------ env
     def reset(self, seeds: Optional[Sequence[int]] = None, mask: Optional[torch.Tensor] = None):
         """ReversiGame() for every (masked) game + np.random.seed(seeds[g]) per game."""
@@ -119,6 +139,11 @@ class Engine:
         m = None if mask is None else mask.to(self.device, torch.uint8).contiguous()
         self._seeds = s.contiguous()
         self._call("rvz_env_reset", ptr(self._seeds), ptr(m) if m is not None else None)
+
+    def reset_device(self, seeds_i32: torch.Tensor, mask_u8: Optional[torch.Tensor] = None):
+        """Graph-capturable reset: persistent int32 seeds / uint8 mask device tensors."""
+        self._stream()
+        self._call("rvz_env_reset", ptr(seeds_i32), ptr(mask_u8) if mask_u8 is not None else None)
 
     def get_state(self):
         """(black int64[G], white int64[G], status int32[G,4]) device tensors (bit patterns)."""

@@ -1,0 +1,182 @@
+"""Batched self-play: the reference's SelfPlay (src/self_play/self_play.py:21-219) over the engine.
+
+``SelfPlayRunner`` advances every game of an ``Engine`` by one ply per call (one MCTS search +
+one move per live game, self_play.py:80-101), optionally captured once into a HIP graph and
+replayed (the 13 select / NN / expand rounds and the act of a ply are one graph launch).
+With ``autoreset`` a finished game restarts at once with the next seed of its slot
+(seed_g, seed_g + G, ...), which keeps every slot busy for steady-state measurement.
+
+``SelfPlay`` is the drop-in for the reference class: same constructor ``(model, args)``, same
+``generate_games(n)`` / ``generate_training_data(n)`` outputs (per-game dict of canonical states,
+action_probs, current_players, values; self_play.py:117-131), with the n games played in
+lockstep instead of one after another.
+"""
+from __future__ import annotations
+
+import os
+import time
+from datetime import datetime
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .engine import Engine, board_canonical
+
+
+class SelfPlayRunner:
+    def __init__(self, engine: Engine, evaluator: Callable, temperature: float = 1.0,
+                 fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
+                 record: bool = False, max_plies: int = 60, seed_stride: int = None):
+        self.eng = engine
+        self.evaluator = evaluator
+        self.temperature = float(temperature)
+        self.fused_softmax = fused_softmax
+        self.autoreset = autoreset
+        self.seed_base = seed_base
+        self.seed_stride = engine.n_games if seed_stride is None else int(seed_stride)
+        self.record = record
+        G, dev = engine.n_games, engine.device
+        self.seeds = (torch.arange(G, dtype=torch.int64, device=dev) + seed_base)
+        self.steps = torch.zeros((), dtype=torch.int64, device=dev)   # committed plies
+        self.games_done = torch.zeros((), dtype=torch.int64, device=dev)
+        self.pre_black = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.pre_white = torch.zeros(G, dtype=torch.int64, device=dev)
+        self.pre_status = torch.zeros(G, 4, dtype=torch.int32, device=dev)
+        self.post_status = torch.zeros(G, 4, dtype=torch.int32, device=dev)
+        self._seed32 = torch.zeros(G, dtype=torch.int32, device=dev)
+        self._mask = torch.zeros(G, dtype=torch.uint8, device=dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        if record:
+            self.rec_black = torch.zeros(max_plies, G, dtype=torch.int64, device=dev)
+            self.rec_white = torch.zeros(max_plies, G, dtype=torch.int64, device=dev)
+            self.rec_side = torch.zeros(max_plies, G, dtype=torch.int32, device=dev)
+            self.rec_idx = torch.full((max_plies, G), -2, dtype=torch.int32, device=dev)
+            self.rec_p = torch.zeros(max_plies, G, engine.npol, dtype=torch.float64, device=dev)
+            self.rec_over = torch.zeros(max_plies, G, 4, dtype=torch.int32, device=dev)
+        self.ply_index = 0
+
+    def start(self):
+        self.eng.reset(self.seeds)
+        self.ply_index = 0
+
+    # one ply for every game; graph-capturable (no host sync)
+    def _body(self):
+        eng = self.eng
+        b, w, st = eng.get_state()
+        self.pre_black.copy_(b)
+        self.pre_white.copy_(w)
+        self.pre_status.copy_(st)
+        eng.search(self.evaluator, fused_softmax=self.fused_softmax)
+        idx, _ = eng.act(self.temperature, apply=True)
+        self.steps += (idx >= 0).sum()
+        _, _, st = eng.get_state()
+        self.post_status.copy_(st)
+        if self.autoreset:
+            self.restart_finished(st)
+
+    def restart_finished(self, status: torch.Tensor):
+        """Restart games that just ended with the next seed of their slot (graph-capturable)."""
+        over = status[:, 1]
+        self.games_done += over.sum()
+        self.seeds += over.to(torch.int64) * self.seed_stride
+        self._mask.copy_(over.to(torch.uint8))
+        self._seed32.copy_(self.seeds.bitwise_and(0xFFFFFFFF).to(torch.int32))
+        self.eng.reset_device(self._seed32, self._mask)
+
+    def capture(self):
+        """Capture one ply into a HIP graph (call after at least one eager ply warmed MIOpen)."""
+        torch.cuda.synchronize(self.eng.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._body()
+        self.graph = g
+        torch.cuda.synchronize(self.eng.device)
+
+    def ply(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._body()
+        if self.record:
+            k = self.ply_index
+            self.rec_black[k].copy_(self.pre_black)
+            self.rec_white[k].copy_(self.pre_white)
+            self.rec_side[k].copy_(self.pre_status[:, 0])
+            self.rec_idx[k].copy_(self.eng.idx_buf)
+            self.rec_p[k].copy_(self.eng.p_buf)
+            self.rec_over[k].copy_(self.post_status)
+        self.ply_index += 1
+
+
+class SelfPlay:
+    """self_play.py:21-219 with the games of one call played in lockstep on the GPU."""
+
+    def __init__(self, model, args: dict):
+        from .network import LeafEvaluator
+        self.model = model
+        self.device = next(model.parameters()).device
+        if self.device.type != "cuda":
+            self.device = torch.device("cuda", torch.cuda.current_device())
+            self.model = model.to(self.device)
+        self.model.eval()
+        self.args = args
+        self.evaluator = LeafEvaluator(self.model, dtype=args.get("nn_dtype", torch.float32),
+                                       device=self.device)
+        self.save_dir = args.get("save_dir", "self_play_data")
+        os.makedirs(self.save_dir, exist_ok=True)
+        self.seed = int(args.get("seed", 42))
+        self.games_played = 0
+
+    def _play(self, num_games: int) -> List[Dict]:
+        eng = Engine(num_games, self.args.get("num_simulations", 800),
+                     self.args.get("batch_size", 64), self.args.get("c_puct", 1.0),
+                     device=self.device)
+        run = SelfPlayRunner(eng, self.evaluator, self.args.get("temperature", 1.0),
+                             fused_softmax=self.args.get("fused_softmax", True),
+                             seed_base=self.seed + self.games_played, record=True)
+        run.start()
+        for _ in range(60):             # every ply places a disc: <= 60 plies per game
+            run.ply()
+        eng.check()
+        G = num_games
+        black, white, side = run.rec_black, run.rec_white, run.rec_side
+        st = torch.stack([side, torch.zeros_like(side), torch.full_like(side, -1),
+                          torch.zeros_like(side)], dim=-1).reshape(-1, 4).contiguous()
+        planes = board_canonical(black.reshape(-1).contiguous(), white.reshape(-1).contiguous(),
+                                 st, eng.board_size).reshape(60, G, 3, eng.board_size,
+                                                             eng.board_size)
+        planes, idx, p = planes.cpu().numpy(), run.rec_idx.cpu().numpy(), run.rec_p.cpu().numpy()
+        side_h, final = side.cpu().numpy(), run.post_status.cpu().numpy()
+        games = []
+        for g in range(G):
+            live = np.flatnonzero(idx[:, g] >= 0)
+            winner = int(final[g, 2]) if final[g, 1] else None
+            players = [int(side_h[k, g]) for k in live]
+            values = [0.0 if winner == 0 else (1.0 if pl == winner else -1.0) for pl in players]
+            games.append({"states": [planes[k, g] for k in live],
+                          "action_probs": [p[k, g] for k in live],
+                          "current_players": players, "values": values, "winner": winner})
+        self.games_played += G
+        return games
+
+    def generate_games(self, num_games: int) -> List[Dict]:
+        t0 = time.time()
+        games = self._play(num_games)
+        stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
+        for i, gd in enumerate(games):
+            rec = {k: gd[k] for k in ("states", "action_probs", "current_players", "values")}
+            torch.save(rec, os.path.join(self.save_dir, f"game_{stamp}_{i}.pt"))
+        print(f"SelfPlay: {num_games} games in {time.time() - t0:.1f}s")
+        return games
+
+    def generate_training_data(self, num_games: int) -> Optional[Dict[str, np.ndarray]]:
+        games = self.generate_games(num_games)
+        states = [s for g in games for s in g["states"]]
+        probs = [p for g in games for p in g["action_probs"]]
+        values = [v for g in games for v in g["values"]]
+        if not states:
+            return None
+        return {"states": np.asarray(states, np.float32),
+                "action_probs": np.asarray(probs, np.float32),
+                "values": np.asarray(values, np.float32).reshape(-1, 1)}

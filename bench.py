@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py — self-play board-steps/sec @ 800 sims/move, 8x8 Reversi (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+A step is one self-play ply of every game on the GPU (one 800-simulation MCTS search + one move
+per game: SelfPlay.generate_games' loop body, self_play.py:80-101). The N = 1 workload is
+BASELINE.json configs[1]: 4,096 games, 800 sims, batch 64, 6-block/64-filter ResNet (random init,
+torch.manual_seed(0)), fp32 evaluator (the reference's precision). Games that end restart at once
+from the next seed of their slot, so every step is a steady-state ply. Multi-GPU: one process per
+GPU, each with its own 4,096 games (weak scaling), no collective in the data path.
+
+Printed on rank 0: one JSON line with value = committed plies of all ranks / max-over-ranks wall
+time, the roofline of the dominant rvz kernel (algorithmic bytes per launch from the kernels' own
+counters / HIP-event average duration, on the launch stream), the NN's MFMA roofline, and the CPU
+baseline (the oracle port + the same net on the host cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "alphazero-reversi_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense peaks, same source
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--games", type=int, default=4096, help="games per GPU")
+    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--blocks", type=int, default=6)
+    ap.add_argument("--filters", type=int, default=64)
+    ap.add_argument("--board", type=int, default=8)
+    ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--instrument-plies", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def make_net(args, device):
+    import rvz
+    torch.manual_seed(0)
+    return rvz.AlphaZeroNetwork(args.board, args.blocks, args.filters).to(device).eval()
+
+
+def instrumented(run, eng, ev, plies):
+    """Eager plies with HIP events around every launch on the launch stream + byte counters."""
+    stream = torch.cuda.current_stream(eng.device)
+    t = {"select": [], "expand_backup": [], "act": [], "nn": []}
+    eng.stats_enable(True)
+
+    def timed(key, fn):
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        r = fn()
+        b.record(stream)
+        t[key].append((a, b))
+        return r
+
+    for _ in range(plies):
+        eng.search_begin()
+        while timed("select", eng.search_step):
+            logits, value = timed("nn", lambda: ev(eng.leaf_x))
+            timed("expand_backup", lambda: eng.search_submit(logits, value, True))
+        timed("act", lambda: eng.act(run.temperature, apply=True))
+        run.restart_finished(eng.get_state()[2])
+    torch.cuda.synchronize(eng.device)
+    sel, exp, act = eng.stats_read()
+    eng.stats_enable(False)
+    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in t.items()}
+    n = {k: len(v) for k, v in t.items()}
+    return ms, n, {"select": sel, "expand_backup": exp, "act": act}
+
+
+def cpu_baseline(args, net):
+    """The oracle port (oracle/, literal reference semantics) + the same net in fp32 on the host
+    cores, from the start position, over a bounded sample of the C2 workload."""
+    from oracle import oracle as O
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cores = max(1, min(cores, os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    cpu_net = make_net(args, "cpu")
+    cpu_net.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
+    G = 64
+    games = [O.new_game(args.board) for _ in range(G)]
+    mts = [O.MT(args.seed + g) for g in range(G)]
+    srch = O.Search(G, args.sims, args.batch, 1.0, bs=args.board)
+    npol = args.board ** 2 + 1
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds and not all(g.over for g in games):
+        srch.begin(games)
+        while (r := srch.step()) is not None:
+            leaves, _ = r
+            x = torch.from_numpy(O.leaf_planes(leaves, args.board))
+            with torch.no_grad():
+                logits, value = cpu_net(x)
+            srch.submit(torch.softmax(logits, 1).numpy(), value.numpy())
+        vis = srch.visits()
+        for g in range(G):
+            if games[g].over:
+                continue
+            nd = O.action_needs_draw(vis[g], 1.0)
+            idx, _, _ = O.action(vis[g], 1.0, mts[g].random_sample() if nd else 0.0)
+            O.make_move(games[g], -1 if idx == npol - 1 else idx, args.board)
+            steps += 1
+    dt = time.perf_counter() - t0
+    # env + tree only: same searches with a zero-cost evaluator (uniform priors, value 0)
+    stub = O.Search(G, args.sims, args.batch, 1.0, bs=args.board)
+    roots = [O.new_game(args.board) for _ in range(G)]
+    u = np.full((G, npol), 1.0 / npol, np.float32)
+    z = np.zeros(G, np.float32)
+    t1 = time.perf_counter()
+    stub.begin(roots)
+    while stub.step() is not None:
+        stub.submit(u, z)
+    dt_stub = time.perf_counter() - t1
+    return {"value": steps / dt, "unit": "board-steps/s", "cores": cores, "kind": "port",
+            "sample": f"{G} games from the start position, {steps} plies in {dt:.1f}s, "
+                      f"{args.sims} sims, oracle/ C search + {args.blocks}x{args.filters} net "
+                      f"fp32 on {cores} host threads",
+            "env_tree_only": {"value": G / dt_stub, "unit": "board-steps/s",
+                              "sample": f"{G} first-ply searches, zero-cost evaluator"}}
+
+
+def main():
+    args = parse()
+    import rvz
+    from rvz import dist as rdist
+
+    rank, local_rank, world = rdist.env_rank_world()
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        rdist.init("nccl")
+    device = torch.device("cuda", local_rank if world > 1 else torch.cuda.current_device())
+    torch.cuda.set_device(device)
+    nn_dtype = torch.float32 if args.nn_dtype == "fp32" else torch.bfloat16
+
+    net = make_net(args, device)
+    ev = rvz.LeafEvaluator(net, dtype=nn_dtype, device=device)
+    eng = rvz.Engine(args.games, args.sims, args.batch, 1.0, board_size=args.board, device=device,
+                     leaf_dtype=torch.float32 if nn_dtype == torch.float32 else torch.bfloat16)
+    first_game = rank * args.games          # global game index space: rank r owns a shard
+    run = rvz.SelfPlayRunner(eng, ev, temperature=1.0, fused_softmax=True, autoreset=True,
+                             seed_base=args.seed + first_game, seed_stride=args.games * world)
+    run.start()
+
+    # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph
+    warm = max(args.warmup, 0 if args.no_graph else 1)
+    for i in range(warm):
+        run.ply()
+        if i == 0 and not args.no_graph:
+            run.capture()
+    torch.cuda.synchronize(device)
+
+    rdist.barrier()
+    torch.cuda.synchronize(device)
+    s0 = int(run.steps.item())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run.ply()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    rdist.barrier()
+    s1 = int(run.steps.item())
+    eng.check()
+    dt = rdist.reduce_max(t1 - t0)
+    total = rdist.reduce_sum(s1 - s0)
+    value = total / dt
+
+    ms, n, bytes_ = instrumented(run, eng, ev, args.instrument_plies)
+    eng.check()
+    kernels = {}
+    for k in ("select", "expand_backup", "act"):
+        per_launch = bytes_[k] / max(1, n[k])
+        kernels[k] = {"avg_us": ms[k] * 1e3, "launches_per_ply": n[k] // args.instrument_plies,
+                      "alg_bytes_per_launch": per_launch,
+                      "achieved_GBs": per_launch / (ms[k] * 1e-3) / 1e9}
+    dom = max(("select", "expand_backup", "act"),
+              key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            traffic = json.load(open(args.pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    nn_flops = ev.flops_per_row() * args.games
+    nn_tflops = nn_flops / (ms["nn"] * 1e-3) / 1e12
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, net)
+
+    if rank == 0:
+        ach = kernels[dom]["achieved_GBs"]
+        out = {
+            "metric": "self-play board-steps/sec @ 800 sims/move, 8x8 Reversi",
+            "value": round(value, 2), "unit": "board-steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64+f32", "data": "synthetic (start position, per-game seeds, random-init net)",
+            "config": {"workload": f"configs[1]: {args.games} games/GPU x {args.sims} sims, "
+                                   f"{args.blocks}x{args.filters} ResNet, {args.board}x{args.board}",
+                       "games_per_gpu": args.games, "global_games": args.games * world,
+                       "sims": args.sims, "batch": args.batch,
+                       "nn": f"{args.blocks}x{args.filters}", "nn_dtype": args.nn_dtype,
+                       "graph": not args.no_graph, "parallelism": f"games sharded x{world}"},
+            "roofline": {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(ach, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic},
+            "kernels": {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()},
+            "nn_roofline": {"bound": "mfma", "achieved": round(nn_tflops, 2),
+                            "peak": MFMA_PEAK_TFLOPS[args.nn_dtype], "unit": "TFLOP/s",
+                            "frac": round(nn_tflops / MFMA_PEAK_TFLOPS[args.nn_dtype], 4),
+                            "avg_ms_per_call": round(ms["nn"], 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

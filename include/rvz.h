@@ -107,6 +107,16 @@ int rvz_act(rvz_engine *e, double temperature, const double *u, int32_t apply, i
 /* ---- introspection (tests / bench) -------------------------------------------------------- */
 /* Host copy of per-engine counters: [0] search batches issued, [1] kernel launches. */
 int rvz_counters(const rvz_engine *e, int64_t *out2 /* host */);
+/* Algorithmic-byte counters (bench roofline): while enabled, every search kernel adds the bytes
+ * its algorithm must move (nodes scanned, planes/rows written, backups) to a device counter;
+ * read returns host int64[3] = {select, expand_backup, act} since the last enable. Off by default
+ * (one atomic per game per launch when on). */
+int rvz_stats_enable(rvz_engine *e, int32_t on);
+int rvz_stats_read(rvz_engine *e, int64_t *out3 /* host */);
+/* Tree export for tests: nodes_out [n_games * nodes_per_game] x {int32 N, f32 W, f32 P, f32 C},
+ * meta_out [n_games * nodes_per_game] uint32 (device). nodes_per_game = rvz_tree_nodes(). */
+int rvz_tree_nodes(const rvz_engine *e);
+int rvz_tree_export(rvz_engine *e, void *nodes_out, uint32_t *meta_out);
 /* Sizes of the engine's device-resident state, for DESIGN/bench accounting (host out). */
 int rvz_footprint(const rvz_engine *e, int64_t *bytes_tree, int64_t *bytes_env);
 

@@ -1,0 +1,227 @@
+"""Search kernels (select / expand_backup / visits / act) through the C-ABI:
+
+ * replay of the reference's recorded games (tests/golden/mcts_*.npz): the engine's leaves must be
+   the reference's NN inputs, and with the reference's own softmax rows and values fed back the
+   visits, the f64 policy vectors (bitwise) and the sampled actions must be the reference's;
+ * lockstep against the literal CPU oracle (no dedup, virtual loss kept) at larger game counts
+   with a real network's outputs shared by both, 8x8 and the 6x6 variant;
+ * full-size (4,096 and 32,768 games) invariants.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_replay as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _status_rows(games):
+    return torch.tensor([[g.side, g.over, g.winner, g.passed] for g in games], dtype=torch.int32)
+
+
+@pytest.mark.parametrize("path", R.fixture_paths(), ids=lambda p: p.split("/")[-1])
+def test_engine_replays_reference_games(path):
+    import rvz
+    fx = R.load(path)
+    games = list(R.games(fx))
+    G, sims, T = len(games), int(fx["sims"]), float(fx["temperature"])
+    eng = rvz.Engine(G, num_simulations=sims, batch_size=int(fx["batch"]),
+                     c_puct=float(fx["c_puct"]))
+    eng.reset([g["seed"] for g in games])
+    ci = [0] * G
+    n_ply = max(len(g["ply_action"]) for g in games)
+    probs = torch.zeros(G, 65, dtype=torch.float32, device="cuda")
+    value = torch.zeros(G, dtype=torch.float32, device="cuda")
+    for k in range(n_ply):
+        b, w, st = eng.get_state()
+        b, st = b.cpu().numpy().view(np.uint64), st.cpu().numpy()
+        for gi, g in enumerate(games):
+            if k < len(g["ply_action"]):
+                assert int(b[gi]) == int(g["ply_black"][k]) and st[gi, 0] == g["ply_side"][k]
+        eng.search_begin()
+        while eng.search_step():
+            need = eng.need.cpu().numpy()
+            x = eng.leaf_x.cpu().numpy()
+            pr = np.zeros((G, 65), np.float32)
+            va = np.zeros(G, np.float32)
+            for gi, g in enumerate(games):
+                if need[gi] == 0:
+                    continue
+                c = ci[gi]
+                assert R.planes_to_masks(x[gi]) == [int(v) for v in g["call_masks"][c]], (k, gi, c)
+                pr[gi], va[gi] = g["call_probs"][c], g["call_value"][c]
+                ci[gi] += 1
+            probs.copy_(torch.from_numpy(pr))
+            value.copy_(torch.from_numpy(va))
+            eng.search_submit(probs, value, is_logits=False)
+        vis = eng.visits().cpu().numpy()
+        idx, p = eng.act(T, apply=True)
+        idx, p = idx.cpu().numpy(), p.cpu().numpy()
+        for gi, g in enumerate(games):
+            if k >= len(g["ply_action"]):
+                assert idx[gi] == -2
+                continue
+            np.testing.assert_array_equal(vis[gi], g["ply_visits"][k])
+            assert np.array_equal(p[gi].view(np.int64), g["ply_p"][k].view(np.int64)), (k, gi)
+            assert idx[gi] == g["ply_action"][k]
+    for gi, g in enumerate(games):
+        assert ci[gi] == len(g["call_ply"])
+    _, _, st = eng.get_state()
+    st = st.cpu().numpy()
+    assert [int(s) for s in st[:, 2]] == [g["winner"] for g in games]
+    eng.check()
+
+
+def _lockstep(oracle, G, sims, bs, n_plies, net, T=1.0, seed0=100, fused=False):
+    """Play n_plies of G games on the engine and on the oracle with shared NN outputs."""
+    import rvz
+    eng = rvz.Engine(G, num_simulations=sims, batch_size=64, board_size=bs)
+    seeds = [seed0 + g for g in range(G)]
+    eng.reset(seeds)
+    srch = oracle.Search(G, sims, 64, 1.0, bs=bs)
+    games = [oracle.new_game(bs) for _ in range(G)]
+    mts = [oracle.MT(s) for s in seeds]
+    npol = bs * bs + 1
+    for k in range(n_plies):
+        srch.begin(games)
+        eng.search_begin()
+        while eng.search_step():
+            r = srch.step()
+            assert r is not None
+            leaves, ncop = r
+            need = eng.need.cpu().numpy()
+            np.testing.assert_array_equal(need, ncop)   # same number of queued copies per game
+            with torch.no_grad():
+                logits, v = net(eng.leaf_x)
+            probs = torch.softmax(logits, dim=1).float().contiguous()
+            v = v.float().contiguous()
+            x = eng.leaf_x.cpu().numpy()
+            for g in np.flatnonzero(need):
+                np.testing.assert_array_equal(x[g], oracle.canonical(leaves[g], bs))
+            if fused:
+                eng.search_submit(logits.float().contiguous(), v, is_logits=True)
+            else:
+                eng.search_submit(probs, v, is_logits=False)
+            srch.submit(probs.cpu().numpy(), v.cpu().numpy())
+        assert srch.step() is None
+        vis_e = eng.visits().cpu().numpy()
+        vis_o = srch.visits()
+        if fused:
+            return vis_e, vis_o
+        np.testing.assert_array_equal(vis_e, vis_o)
+        idx, p = eng.act(T, apply=True)
+        idx, p = idx.cpu().numpy(), p.cpu().numpy()
+        for g in range(G):
+            if games[g].over:
+                assert idx[g] == -2
+                continue
+            u = mts[g].random_sample() if oracle.action_needs_draw(vis_o[g], T) else 0.0
+            oi, op, _ = oracle.action(vis_o[g], T, u)
+            assert oi == idx[g], (k, g)
+            assert np.array_equal(op.view(np.int64), p[g].view(np.int64))
+            oracle.make_move(games[g], -1 if oi == npol - 1 else oi, bs)
+        b, w, st = eng.get_state()
+        b, w, st = b.cpu().numpy().view(np.uint64), w.cpu().numpy().view(np.uint64), st.cpu().numpy()
+        for g in range(G):
+            assert (int(b[g]), int(w[g]), *map(int, st[g])) == \
+                (games[g].black, games[g].white, games[g].side, games[g].over,
+                 games[g].winner, games[g].passed)
+    eng.check()
+    return None
+
+
+def _net(bs, blocks=2, filters=32, seed=0):
+    import rvz
+    torch.manual_seed(seed)
+    net = rvz.AlphaZeroNetwork(board_size=bs, num_res_blocks=blocks, num_filters=filters).cuda().eval()
+    return lambda x: net(x.float())
+
+
+def test_lockstep_vs_oracle_8x8_full_games(oracle):
+    _lockstep(oracle, G=48, sims=800, bs=8, n_plies=60, net=_net(8))
+
+
+def test_lockstep_vs_oracle_8x8_s100_t05(oracle):
+    _lockstep(oracle, G=64, sims=100, bs=8, n_plies=60, net=_net(8, seed=3), T=0.5, seed0=7)
+
+
+def test_lockstep_vs_oracle_6x6(oracle):
+    _lockstep(oracle, G=64, sims=400, bs=6, n_plies=32, net=_net(6, seed=1))
+
+
+def test_fused_softmax_within_tolerance():
+    """The expand kernel's fused softmax vs torch.softmax (mcts.py:596): priors to rtol 2e-6."""
+    import rvz
+    G = 256
+    eng = rvz.Engine(G, num_simulations=64, batch_size=64)
+    eng.reset(range(G))
+    eng.search_begin()
+    assert eng.search_step()
+    torch.manual_seed(0)
+    logits = (torch.randn(G, 65, device="cuda") * 3).contiguous()
+    eng.search_submit(logits, torch.zeros(G, device="cuda"), is_logits=True)
+    nodes, meta = eng.tree()
+    torch.cuda.synchronize()
+    eng.check()
+    pri = nodes[:, 1:5, 2].cpu().view(torch.float32).numpy()    # root children (4 legal moves)
+    sq = (meta[:, 1:5].cpu().numpy() & 63)
+    ref = torch.softmax(logits, 1).cpu().numpy()
+    np.testing.assert_array_equal(sq[0], [19, 26, 37, 44])
+    np.testing.assert_allclose(pri, np.take_along_axis(ref, sq, 1), rtol=2e-6, atol=0)
+
+
+def test_full_size_invariants_4096():
+    """C2 size: one full 800-sim ply over 4,096 games with the 6x64 net (fp32)."""
+    import rvz
+    G = 4096
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
+    ev = rvz.LeafEvaluator(net)
+    eng = rvz.Engine(G, num_simulations=800, batch_size=64)
+    eng.reset(range(42, 42 + G))
+    eng.search(ev)
+    vis = eng.visits()
+    idx, p = eng.act(1.0, apply=True)
+    torch.cuda.synchronize()
+    eng.check()
+    v = vis.cpu().numpy()
+    assert (v.sum(1) == 800 - 64).all()            # root absorbs the first batch itself
+    pp = p.cpu().numpy()
+    assert np.allclose(pp.sum(1), 1.0, atol=1e-12)
+    ii = idx.cpu().numpy()
+    assert ((ii >= 0) & (ii < 64)).all()
+    assert (v[np.arange(G), ii] > 0).all()          # sampled moves were visited
+    # all games start from the same position: the 4 legal first moves only
+    assert set(np.unique(ii)) <= {19, 26, 37, 44}
+
+
+def test_full_size_invariants_32768():
+    """C3 size (32,768 games, 800 sims): a full ply with a cheap evaluator; no device errors."""
+    import rvz
+    G = 32768
+    eng = rvz.Engine(G, num_simulations=800, batch_size=64)
+    eng.reset(range(G))
+    zl = torch.zeros(G, 65, device="cuda")
+    zv = torch.zeros(G, device="cuda")
+    for ply in range(3):
+        eng.search(lambda x: (zl, zv))
+        idx, p = eng.act(1.0, apply=True)
+    torch.cuda.synchronize()
+    eng.check()
+    vis = eng.visits().cpu().numpy()
+    assert (vis.sum(1) == 736).all()
+
+
+def test_bf16_leaf_planes_equal_f32():
+    import rvz
+    G = 512
+    a = rvz.Engine(G, 128, 64, leaf_dtype=torch.float32)
+    b = rvz.Engine(G, 128, 64, leaf_dtype=torch.bfloat16)
+    for e in (a, b):
+        e.reset(range(G))
+        e.search_begin()
+        assert e.search_step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.leaf_x, b.leaf_x.float())
+    assert torch.equal(a.need, b.need)
