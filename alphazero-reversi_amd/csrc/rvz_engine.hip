@@ -80,12 +80,12 @@ struct View {  // kernel argument: device pointers + sizes
     int32_t* pend;
     int32_t* plen;
     uint64_t* leaf_legal;
+    uint64_t* root_legal;  // [G] legal mask of the current search's root (its children's squares)
     int32_t* nexp;
-    const float* sqrt_tab;  // [sims + 1]
     double* rng_u;          // [G][RNG_DRAWS]
     int32_t* rng_pos;
     int32_t* err;
-    unsigned long long* stats;  // [4] algorithmic bytes: select, expand_backup, act, launches; or null
+    unsigned long long* stats;  // [3][G] algorithmic bytes per game: k_step, k_act, k_expand_backup; or null
 };
 
 enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4 };
@@ -137,12 +137,15 @@ __device__ __forceinline__ int wave_argmax_first(float s, bool valid, int lane) 
 }
 
 // ---- backup (mcts.py:625-640): lane j updates path node plen-1-j; `copies` sequential adds ----
-__device__ __forceinline__ void backup_path(Node* nodes, int mypath, int plen, float value,
-                                            int copies, int lane) {
+// path_reg: lane i holds the i-th node of the path (root = lane 0). Returns the updated visit
+// count of the root in every lane.
+__device__ __forceinline__ int backup_path(Node* nodes, int path_reg, int plen, float value,
+                                           int copies, int lane) {
     // order this wave's earlier node stores (UCB caches) before the read-modify-write below
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     const int j = plen - 1 - lane;  // lane's path index counted from the root
-    const int nid = __shfl(mypath, j < 0 ? 0 : j);
+    const int nid = __shfl(path_reg, j < 0 ? 0 : j);
+    int n_after = 0;
     if (lane < plen) {
         const float sv = (lane & 1) ? -value : value;  // sign = +1 at the leaf, then alternates
         Node nd = nodes[nid];
@@ -152,35 +155,93 @@ __device__ __forceinline__ void backup_path(Node* nodes, int mypath, int plen, f
         nd.w = w;
         nd.c = __int_as_float(0x7fc00000);  // del cached_ucb
         nodes[nid] = nd;
+        n_after = nd.n;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    return __shfl(n_after, plen - 1);  // the lane that updated the root
 }
 
 // UCB of an expanded child whose score is not cached (mcts.py:102-114); turn_c = child's turn.
-__device__ __forceinline__ float ucb_score(const Node& c, int parent_n, int turn_c, float cpuct,
-                                           const float* sqrt_tab) {
+// sqrt: the device f64 sqrt is correctly rounded (tests/test_gpu_numerics.py), so this is
+// exactly `np.float32(math.sqrt(parent_visit_count))` as the reference's NumPy promotion takes it.
+__device__ __forceinline__ float ucb_score(const Node& c, float sqrt_np, int turn_c, float cpuct) {
     float u = cpuct * c.p;
-    u = u * sqrt_tab[parent_n];
+    u = u * sqrt_np;
     u = u / (float)(1 + c.n);
     float q = c.w / (float)(c.n > 1 ? c.n : 1);
     if (turn_c != 1) q = -q;
     return q + u;
 }
 
-// ---- search kernels -----------------------------------------------------------------------------
+// expand + backup of the queued leaf: _process_batch pass 2 (mcts.py:600-623) and
+// MCTSNode.expand (:141-161). Returns the root's visit count after the backup (-1: nothing to do).
+template <int BS>
+__device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lane,
+                                                   const float* __restrict__ policy,
+                                                   int is_logits, const float* __restrict__ value,
+                                                   unsigned long long& ab) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    const int copies = v.pend[g];
+    if (copies == 0) return -1;
+    const int plen = v.plen[g];
+    const int path_reg = lane < plen ? v.path[g * PATH_CAP + lane] : 0;
+    const uint64_t V = v.leaf_legal[g];
+    const int e = v.nexp[g];
+    const float val = value[g];
+    const float* row = policy + (size_t)g * NPOL;
+    float prob = lane < NSQ ? row[lane] : 0.0f;
+    const float xpass = row[NSQ];
+    const int leaf = __shfl(path_reg, plen - 1);
+    Node* nodes = v.nodes + (size_t)g * v.M;
+    uint32_t* meta = v.meta + (size_t)g * v.M;
+    const uint32_t lm = meta[leaf];
+    if (is_logits) {  // F.softmax(policy_logits, dim=1) over all S*S+1 outputs (mcts.py:596)
+        const float mx = fmaxf(wave_max_f(lane < NSQ ? prob : -INFINITY), xpass);
+        const float ex = lane < NSQ ? expf(prob - mx) : 0.0f;
+        const float denom = wave_sum_f(ex) + expf(xpass - mx);
+        prob = ex / denom;
+    }
+    const int base = 1 + e * NSQ;
+    if (base + NSQ > v.M) {
+        if (lane == 0) atomicOr(v.err, ERR_POOL);
+        return -1;
+    }
+    if (lane < NSQ && ((V >> lane) & 1ull)) {
+        const int idx = __popcll(V & ((1ull << lane) - 1ull));
+        Node c;
+        c.n = 0; c.w = 0.0f; c.p = prob; c.c = __int_as_float(0x7fc00000);
+        nodes[base + idx] = c;
+        meta[base + idx] = meta_pack(lane, 3 - m_turn(lm));
+    }
+    if (lane == 0) {
+        meta[leaf] = lm | ((uint32_t)__popcll(V) << 11) | ((uint32_t)e << 18);
+        v.nexp[g] = e + 1;
+        v.pend[g] = 0;
+    }
+    const int root_n = backup_path(nodes, path_reg, plen, val, copies, lane);
+    if (v.stats) {
+        // pend/plen/path/legal/nexp reads, policy row + value, leaf meta r/w, children, backup
+        const unsigned long long nch = (unsigned long long)__popcll(V);
+        ab += 8ull + 4ull * plen + 8 + 4 + 4ull * NPOL + 4 + 8 + 20ull * nch + 32ull * plen + 4;
+    }
+    return root_n;
+}
+
 // select: mcts.py:348-386 for one batch of `bsz` traversals + _process_batch pass 1 (:561-585).
+// root_n_known >= 0: the root's visit count is already in registers (fused after a backup).
 template <int BS, typename XT>
-__global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* __restrict__ leaf_x,
-                                                int32_t* __restrict__ need) {
+__device__ __forceinline__ void select_phase(const View& v, int g, int lane, int first, int bsz,
+                                             int root_n_known, XT* __restrict__ leaf_x,
+                                             int32_t* __restrict__ need, unsigned long long& ab) {
     constexpr int NSQ = Geo<BS>::NSQ;
-    const int lane = threadIdx.x & 63;
-    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
-    if (g >= v.G) return;
     Node* nodes = v.nodes + (size_t)g * v.M;
     uint32_t* meta = v.meta + (size_t)g * v.M;
     const GameS root = load_game(v, g);
     uint32_t root_meta;
+    int root_n;
     if (first) {  // new root (mcts.py:334-341): prior 1.0, turn = side to move
         root_meta = meta_pack(0, root.side);
+        root_n = 0;
         if (lane == 0) {
             Node r;
             r.n = 0; r.w = 0.0f; r.p = 1.0f; r.c = __int_as_float(0x7fc00000);
@@ -188,66 +249,77 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
             meta[0] = root_meta;
             v.nexp[g] = 0;
         }
+        const uint64_t rl = root.over ? 0ull : legal_wave<BS>(mine(root), theirs(root), lane);
+        if (lane == 0) v.root_legal[g] = rl;
+        ab += 20 + 8;
     } else {
         root_meta = meta[0];
+        root_n = root_n_known >= 0 ? root_n_known : nodes[0].n;
+        ab += 4 + (root_n_known >= 0 ? 0 : 4);
     }
-    int copies = 0, plen = 0, mypath = 0;
-    unsigned long long ab = 32 + (first ? 20 : 4);  // game state read; root node/meta
+    ab += 32;  // game state
+    int copies = 0, plen = 0, path_reg = 0;
     if (!root.over) {
         int remaining = bsz;
         for (;;) {
             GameS sim = root;
-            int node = 0, depth = 0;
+            int depth = 0, node = 0, parent_n = root_n;
             uint32_t m = root_meta;
-            mypath = 0;  // lane 0 holds the root
+            path_reg = 0;  // lane 0 holds the root
             for (;;) {
                 const int nch = m_nchild(m);
                 if (m_term(m) || nch == 0) break;  // while node.expanded() and not terminal
-                const int parent_n = nodes[node].n;
                 const int base = 1 + m_block(m) * NSQ;
-                float score = 0.0f;
+                // one round trip per level: the children's node rows and meta words together
+                Node c;
+                uint32_t cm = 0;
                 if (lane < nch) {
-                    const Node c = nodes[base + lane];
+                    c = nodes[base + lane];
+                    cm = meta[base + lane];
+                } else {
+                    c.n = 0; c.w = 0.0f; c.p = 0.0f; c.c = 0.0f;
+                }
+                float score = 0.0f;
+                bool wrote = false;
+                if (lane < nch) {
                     if (c.n == 0) {
                         score = INFINITY;
                     } else if (!isnan(c.c)) {
                         score = c.c;
                     } else {
-                        score = ucb_score(c, parent_n, 3 - m_turn(m), v.cpuct, v.sqrt_tab);
+                        const float sq_np = (float)sqrt((double)parent_n);
+                        score = ucb_score(c, sq_np, 3 - m_turn(m), v.cpuct);
                         nodes[base + lane].c = score;
+                        wrote = true;
                     }
                 }
                 const int ci = wave_argmax_first(score, lane < nch, lane);
-                if (v.stats) {  // parent N, the children's nodes, the chosen child's meta, cache writes
-                    const int nw = __popcll(__ballot(lane < nch && score == score &&
-                                                     !isinf(score)));
-                    ab += 4 + 16ull * nch + 4 + 4ull * nw;
-                }
+                if (v.stats) ab += 16ull * nch + 4ull * nch + 4ull * __popcll(__ballot(wrote));
                 node = base + ci;
-                m = meta[node];
-                make_move<BS>(sim, m_sq(m));
+                m = (uint32_t)__shfl((int)cm, ci);
+                parent_n = __shfl(c.n, ci);
+                make_move_wave<BS>(sim, m_sq(m), lane);
                 ++depth;
                 if (depth >= PATH_CAP) {  // unreachable when ceil(sims/batch) <= 64 (checked)
                     if (lane == 0) atomicOr(v.err, ERR_PATH);
                     depth = PATH_CAP - 1;
                     break;
                 }
-                if (lane == depth) mypath = node;
+                if (lane == depth) path_reg = node;
             }
             if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
-                backup_path(nodes, mypath, depth + 1, m_tv(m), 1, lane);
+                root_n = backup_path(nodes, path_reg, depth + 1, m_tv(m), 1, lane);
                 ab += 32ull * (depth + 1);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                 if (--remaining == 0) break;
                 continue;
             }
             // pass 1: valid moves of the leaf's simulated game
-            const uint64_t V = legal<BS>(mine(sim), theirs(sim));
+            const uint64_t V = legal_wave<BS>(mine(sim), theirs(sim), lane);
             if (V == 0ull) {  // terminal, BLACK-absolute value from get_winner() (mcts.py:567-579)
                 const int w = sim.over ? sim.winner : -1;
                 const uint32_t code = w == 1 ? 1u : (w == 2 ? 2u : 0u);
                 if (lane == 0) meta[node] = m | (1u << 8) | (code << 9);
-                backup_path(nodes, mypath, depth + 1, w == 1 ? 1.0f : (w == 2 ? -1.0f : 0.0f),
+                backup_path(nodes, path_reg, depth + 1, w == 1 ? 1.0f : (w == 2 ? -1.0f : 0.0f),
                             remaining, lane);
                 ab += 4 + 32ull * (depth + 1);
                 break;
@@ -262,7 +334,7 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
                 row[NSQ + lane] = (XT)(float)((O >> lane) & 1ull);
                 row[2 * NSQ + lane] = (XT)(float)((V >> lane) & 1ull);
             }
-            if (lane < plen) v.path[g * PATH_CAP + lane] = mypath;
+            if (lane < plen) v.path[g * PATH_CAP + lane] = path_reg;
             if (lane == 0) v.leaf_legal[g] = V;
             ab += 3ull * NSQ * sizeof(XT) + 4ull * plen + 8;
             break;
@@ -272,74 +344,49 @@ __global__ __launch_bounds__(256) void k_select(View v, int first, int bsz, XT* 
         need[g] = copies;
         v.pend[g] = copies;
         v.plen[g] = plen;
-        if (v.stats) atomicAdd(&v.stats[0], ab + 12);
     }
+    ab += 12;
 }
 
-// expand + backup: _process_batch pass 2 (mcts.py:600-623) and MCTSNode.expand (:141-161).
+// One search round: the previous batch's expand + backup (when a submit is pending), then the
+// next batch's selection, in one launch (one wave per game).
+template <int BS, typename XT>
+__global__ __launch_bounds__(256) void k_step(View v, int expand, const float* __restrict__ policy,
+                                              int is_logits, const float* __restrict__ value,
+                                              int first, int bsz, XT* __restrict__ leaf_x,
+                                              int32_t* __restrict__ need) {
+    const int lane = threadIdx.x & 63;
+    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (g >= v.G) return;
+    unsigned long long ab_e = 0, ab_s = 0;
+    int root_n = -1;
+    if (expand) root_n = expand_backup_phase<BS>(v, g, lane, policy, is_logits, value, ab_e);
+    select_phase<BS, XT>(v, g, lane, first, bsz, root_n, leaf_x, need, ab_s);
+    if (v.stats && lane == 0) v.stats[g] += ab_s + ab_e;  // per-game slot: no contention
+}
+
 template <int BS>
 __global__ __launch_bounds__(256) void k_expand_backup(View v, const float* __restrict__ policy,
                                                        int is_logits,
                                                        const float* __restrict__ value) {
-    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (g >= v.G) return;
-    const int copies = v.pend[g];
-    if (copies == 0) return;
-    const int plen = v.plen[g];
-    const int mypath = lane < plen ? v.path[g * PATH_CAP + lane] : 0;
-    const int leaf = __shfl(mypath, plen - 1);
-    Node* nodes = v.nodes + (size_t)g * v.M;
-    uint32_t* meta = v.meta + (size_t)g * v.M;
-    const uint64_t V = v.leaf_legal[g];
-    const float* row = policy + (size_t)g * NPOL;
-    float prob = lane < NSQ ? row[lane] : 0.0f;
-    if (is_logits) {  // F.softmax(policy_logits, dim=1) over all S*S+1 outputs (mcts.py:596)
-        const float xpass = row[NSQ];
-        const float mx = fmaxf(wave_max_f(lane < NSQ ? prob : -INFINITY), xpass);
-        const float e = lane < NSQ ? expf(prob - mx) : 0.0f;
-        const float denom = wave_sum_f(e) + expf(xpass - mx);
-        prob = e / denom;
-    }
-    const uint32_t lm = meta[leaf];
-    const int e = v.nexp[g];
-    const int base = 1 + e * NSQ;
-    if (base + NSQ > v.M) {
-        if (lane == 0) atomicOr(v.err, ERR_POOL);
-        return;
-    }
-    if (lane < NSQ && ((V >> lane) & 1ull)) {
-        const int idx = __popcll(V & ((1ull << lane) - 1ull));
-        Node c;
-        c.n = 0; c.w = 0.0f; c.p = prob; c.c = __int_as_float(0x7fc00000);
-        nodes[base + idx] = c;
-        meta[base + idx] = meta_pack(lane, 3 - m_turn(lm));
-    }
-    if (lane == 0) {
-        meta[leaf] = lm | ((uint32_t)__popcll(V) << 11) | ((uint32_t)e << 18);
-        v.nexp[g] = e + 1;
-        v.pend[g] = 0;
-    }
-    backup_path(nodes, mypath, plen, value[g], copies, lane);
-    if (v.stats && lane == 0) {
-        // pend/plen/path/legal/nexp reads, policy row + value, leaf meta r/w, children, backup
-        const unsigned long long nch = (unsigned long long)__popcll(V);
-        atomicAdd(&v.stats[1], 8ull + 4ull * plen + 8 + 8 + 4ull * NPOL + 4 + 8 + 20ull * nch +
-                                   32ull * plen + 4);
-    }
+    unsigned long long ab = 0;
+    expand_backup_phase<BS>(v, g, lane, policy, is_logits, value, ab);
+    if (v.stats && lane == 0) v.stats[2 * (size_t)v.G + g] += ab;
 }
 
 // Dense visit count of square `lane` at the root: the root's children are the set bits of the
-// root board's legal mask in ascending order (expand inserts them row-major).
+// search root's legal mask in ascending order (expand inserts them row-major).
 template <int BS>
-__device__ __forceinline__ int root_visits(const View& v, int g, const GameS& root, int lane) {
+__device__ __forceinline__ int root_visits(const View& v, int g, int lane) {
     constexpr int NSQ = Geo<BS>::NSQ;
     const Node* nodes = v.nodes + (size_t)g * v.M;
     const uint32_t m0 = v.meta[(size_t)g * v.M];
+    const uint64_t V = v.root_legal[g];
     const int nch = m_nchild(m0);
     if (nch == 0 || lane >= NSQ) return 0;
-    const uint64_t V = legal<BS>(mine(root), theirs(root));
     if (!((V >> lane) & 1ull)) return 0;
     const int idx = __popcll(V & ((1ull << lane) - 1ull));
     return nodes[1 + m_block(m0) * NSQ + idx].n;
@@ -351,8 +398,7 @@ __global__ __launch_bounds__(256) void k_visits(View v, int32_t* __restrict__ ou
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (g >= v.G) return;
-    const GameS root = load_game(v, g);
-    const int n = root_visits<BS>(v, g, root, lane);
+    const int n = root_visits<BS>(v, g, lane);
     if (lane < NSQ) out[(size_t)g * NPOL + lane] = n;
     if (lane == 0) out[(size_t)g * NPOL + NSQ] = 0;  // no pass child is ever created
 }
@@ -367,62 +413,72 @@ __device__ __forceinline__ double np_power(double x, double e) {
     return pow(x, e);
 }
 
-// np.sum over [t_0 .. t_{NSQ-1}, tpass] in numpy's pairwise order (8 accumulators, n <= 128).
-template <int NPOL>
-__device__ __forceinline__ double np_pairwise_sum(double t, double tpass) {
-    static_assert(NPOL >= 8 && NPOL <= 128, "pairwise_sum block");
-    constexpr int NMAIN = NPOL - NPOL % 8;
-    auto at = [&](int i) -> double { return i == NPOL - 1 ? tpass : __shfl(t, i); };
-    double r[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = at(j);
-    for (int i = 8; i < NMAIN; i += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) r[j] += at(i + j);
-    }
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (int i = NMAIN; i < NPOL; ++i) res += at(i);
-    return res;
-}
-
-// act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action).
+// act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action); optionally preceded
+// by the last batch's pending expand + backup.
 template <int BS>
-__global__ __launch_bounds__(256) void k_act(View v, double temperature, const double* __restrict__ uo,
+__global__ __launch_bounds__(256) void k_act(View v, int expand, const float* __restrict__ policy,
+                                             int is_logits, const float* __restrict__ value,
+                                             double temperature, const double* __restrict__ uo,
                                              int apply, int32_t* __restrict__ out_idx,
                                              double* __restrict__ out_p) {
     constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
-    const int lane = threadIdx.x & 63;
-    const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
+    constexpr int NMAIN = NPOL - NPOL % 8;
+    __shared__ double sp[WPB][NPOL + 7];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = blockIdx.x * WPB + wid;
     if (g >= v.G) return;
+    unsigned long long ab = 0;
+    if (expand) expand_backup_phase<BS>(v, g, lane, policy, is_logits, value, ab);
     GameS gm = load_game(v, g);
     double* prow = out_p + (size_t)g * NPOL;
     if (gm.over) {
         if (lane < NSQ) prow[lane] = 0.0;
-        if (lane == 0) { prow[NSQ] = 0.0; out_idx[g] = -2; }
+        if (lane == 0) {
+            prow[NSQ] = 0.0;
+            out_idx[g] = -2;
+            if (v.stats) v.stats[(size_t)v.G + g] += ab + 32 + 8ull * NPOL + 4;
+        }
         return;
     }
-    const int n = root_visits<BS>(v, g, gm, lane);
+    const int n = root_visits<BS>(v, g, lane);
     const int total = wave_sum_i(n);
     double p = (lane < NSQ && total > 0) ? (double)n / (double)total : 0.0;
     double ppass = 0.0;
+    double* s = sp[wid];
     if (temperature > 0.0 && __any(p != 0.0)) {
         const double ex = 1.0 / temperature;
         const double t = lane < NSQ ? np_power(p, ex) : 0.0;
         const double tp = np_power(0.0, ex);
-        const double s = np_pairwise_sum<NPOL>(t, tp);
-        p = t / s;
-        ppass = tp / s;
+        // np.sum in numpy's pairwise order: 8 accumulators over the first NMAIN entries, then tail
+        if (lane < NSQ) s[lane] = t;
+        if (lane == 0) s[NSQ] = tp;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        double r = 0.0;
+        if (lane < 8) {
+            r = s[lane];
+            for (int i = 8 + lane; i < NMAIN; i += 8) r += s[i];
+        }
+        const double r0 = __shfl(r, 0), r1 = __shfl(r, 1), r2 = __shfl(r, 2), r3 = __shfl(r, 3);
+        const double r4 = __shfl(r, 4), r5 = __shfl(r, 5), r6 = __shfl(r, 6), r7 = __shfl(r, 7);
+        double sum = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+        for (int i = NMAIN; i < NPOL; ++i) sum += s[i];
+        p = t / sum;
+        ppass = tp / sum;
+        __builtin_amdgcn_wave_barrier();
     }
     const bool all_zero = !__any(lane < NSQ && p != 0.0) && ppass == 0.0;
-    int idx;
+    if (lane < NSQ) s[lane] = p;
+    if (lane == 0) s[NSQ] = ppass;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    int idx = 0;
     if (temperature == 0.0 || all_zero) {  // np.argmax: first maximum
-        double best = ppass;  // compared last: a square wins ties
-        int bi = NSQ;
-        for (int i = NSQ - 1; i >= 0; --i) {
-            const double pi = __shfl(p, i);
-            if (pi >= best) { best = pi; bi = i; }
+        if (lane == 0) {
+            double best = s[0];
+            for (int i = 1; i < NPOL; ++i)
+                if (s[i] > best) { best = s[i]; idx = i; }
         }
-        idx = bi;
     } else {  // np.random.choice(NPOL, p=p): cumsum, /= last, searchsorted(u, 'right')
         double u;
         if (uo) {
@@ -437,28 +493,30 @@ __global__ __launch_bounds__(256) void k_act(View v, double temperature, const d
             }
             if (lane == 0) v.rng_pos[g] = pos + 1;
         }
-        double acc = 0.0;  // cdf[-1]: the same sequential adds as p.cumsum()
-        for (int i = 0; i < NPOL; ++i) acc += (i < NSQ) ? __shfl(p, i) : ppass;
-        const double last = acc;
-        acc = 0.0;
-        idx = 0;
-        for (int i = 0; i < NPOL; ++i) {
-            acc += (i < NSQ) ? __shfl(p, i) : ppass;
-            if (acc / last <= u) idx = i + 1;  // count of cdf entries <= u
+        if (lane == 0) {
+            double acc = 0.0;  // cdf[-1]: the same sequential adds as p.cumsum()
+            for (int i = 0; i < NPOL; ++i) acc += s[i];
+            const double last = acc;
+            acc = 0.0;
+            for (int i = 0; i < NPOL; ++i) {
+                acc += s[i];
+                if (acc / last <= u) idx = i + 1;  // count of cdf entries <= u
+            }
         }
     }
+    idx = __shfl(idx, 0);
     if (lane < NSQ) prow[lane] = p;
     if (lane == 0) {
         prow[NSQ] = ppass;
         out_idx[g] = idx;
     }
     if (apply) {
-        make_move<BS>(gm, idx == NSQ ? -1 : idx);  // (row, col) = (-1, -1) for the pass index
+        make_move_wave<BS>(gm, idx == NSQ ? -1 : idx, lane);  // (-1, -1) for the pass index
         if (lane == 0) store_game(v, g, gm);
     }
     if (v.stats && lane == 0)  // state r/(w), root meta + children N, p row + idx, rng
-        atomicAdd(&v.stats[2], 32ull + (apply ? 32 : 0) + 4 + 4ull * m_nchild(v.meta[(size_t)g * v.M]) +
-                                   8ull * NPOL + 4 + 16);
+        v.stats[(size_t)v.G + g] += ab + 32ull + (apply ? 32 : 0) + 12 +
+                                    4ull * m_nchild(v.meta[(size_t)g * v.M]) + 8ull * NPOL + 4 + 16;
 }
 
 // reset: new game (board.py:25-39) + np.random.seed(seed) random_sample() stream.
@@ -472,10 +530,10 @@ __global__ __launch_bounds__(256) void k_reset(View v, const uint32_t* __restric
     if (mask && !mask[g]) return;
     uint32_t* k = key[wid];
     if (lane == 0) {  // mt19937_seed (init_genrand): inherently sequential
-        uint32_t s = seeds[g];
+        uint32_t sd = seeds[g];
         for (int pos = 0; pos < 624; ++pos) {
-            k[pos] = s;
-            s = 1812433253u * (s ^ (s >> 30)) + (uint32_t)(pos + 1);
+            k[pos] = sd;
+            sd = 1812433253u * (sd ^ (sd >> 30)) + (uint32_t)(pos + 1);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -493,11 +551,11 @@ __global__ __launch_bounds__(256) void k_reset(View v, const uint32_t* __restric
     const uint32_t a = word(2 * lane) >> 5, b = word(2 * lane + 1) >> 6;
     v.rng_u[(size_t)g * RNG_DRAWS + lane] = ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
     if (lane == 0) {
-        GameS s;
-        s.black = Geo<BS>::START_BLACK;
-        s.white = Geo<BS>::START_WHITE;
-        s.side = 1; s.over = 0; s.winner = -1; s.passed = 0;
-        store_game(v, g, s);
+        GameS st;
+        st.black = Geo<BS>::START_BLACK;
+        st.white = Geo<BS>::START_WHITE;
+        st.side = 1; st.over = 0; st.winner = -1; st.passed = 0;
+        store_game(v, g, st);
         v.rng_pos[g] = 0;
         v.pend[g] = 0;
     }
@@ -563,6 +621,11 @@ struct rvz_engine {
     hipStream_t stream = nullptr;
     int next_batch = 0;  // batches issued in the current search
     int searching = 0;
+    // a submitted batch whose expand + backup runs at the start of the next launch (k_step/k_act)
+    int pending = 0;
+    const float* pend_policy = nullptr;
+    const float* pend_value = nullptr;
+    int pend_is_logits = 0;
     int64_t counters[2] = {0, 0};
     View v;
     unsigned long long* stats_buf = nullptr;
@@ -649,23 +712,20 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     v.pend = dalloc<int32_t>(e, G);
     v.plen = dalloc<int32_t>(e, G);
     v.leaf_legal = dalloc<uint64_t>(e, G);
+    v.root_legal = dalloc<uint64_t>(e, G);
     v.nexp = dalloc<int32_t>(e, G);
-    float* sqrt_tab = dalloc<float>(e, (size_t)cfg->num_simulations + 1);
-    v.sqrt_tab = sqrt_tab;
     v.rng_u = dalloc<double>(e, (size_t)G * RNG_DRAWS);
     v.rng_pos = dalloc<int32_t>(e, G);
     v.err = dalloc<int32_t>(e, 1);
-    e->stats_buf = dalloc<unsigned long long>(e, 4);
+    e->stats_buf = dalloc<unsigned long long>(e, 3 * (size_t)G);
     v.stats = nullptr;
     for (void* p : e->allocs)
         if (!p) { g_create_error = "hipMalloc failed (out of device memory?)"; rvz_destroy(e); return RVZ_ENOMEM; }
-    std::vector<float> tab((size_t)cfg->num_simulations + 1);
-    for (size_t n = 0; n < tab.size(); ++n) tab[n] = (float)sqrt((double)n);  // math.sqrt -> f32
-    hipError_t s = hipMemcpy(sqrt_tab, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice);
-    s = s == hipSuccess ? hipMemset(v.err, 0, sizeof(int32_t)) : s;
+    hipError_t s = hipMemset(v.err, 0, sizeof(int32_t));
     s = s == hipSuccess ? hipMemset(v.pend, 0, sizeof(int32_t) * G) : s;
     s = s == hipSuccess ? hipMemset(v.rng_pos, 0, sizeof(int32_t) * G) : s;
     s = s == hipSuccess ? hipMemset(v.meta, 0, sizeof(uint32_t) * (size_t)G * e->M) : s;
+    s = s == hipSuccess ? hipMemset(v.root_legal, 0, sizeof(uint64_t) * G) : s;
     if (s == hipSuccess) s = hipDeviceSynchronize();
     if (s != hipSuccess) {
         g_create_error = std::string("device init: ") + hipGetErrorString(s);
@@ -724,6 +784,7 @@ int rvz_check(rvz_engine* e, int32_t* host_err) {
 
 int rvz_env_reset(rvz_engine* e, const uint32_t* seeds, const uint8_t* mask) {
     if (!e || !seeds) return RVZ_EINVAL;
+    e->pending = 0;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
     if (e->BS == 8) hipLaunchKernelGGL(k_reset<8>, grid, block, 0, e->stream, e->v, seeds, mask);
     else hipLaunchKernelGGL(k_reset<6>, grid, block, 0, e->stream, e->v, seeds, mask);
@@ -742,6 +803,7 @@ int rvz_env_get(rvz_engine* e, uint64_t* black, uint64_t* white, int32_t* status
 
 int rvz_env_set(rvz_engine* e, const uint64_t* black, const uint64_t* white, const int32_t* status) {
     if (!e || !black || !white || !status) return RVZ_EINVAL;
+    e->pending = 0;
     const size_t G = e->v.G;
     RVZ_HIP(hipMemcpyAsync(e->v.black, black, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
     RVZ_HIP(hipMemcpyAsync(e->v.white, white, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
@@ -805,6 +867,7 @@ int rvz_search_begin(rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
     e->next_batch = 0;
     e->searching = 1;
+    e->pending = 0;  // an unconsumed submit of an abandoned search is dropped
     return RVZ_OK;
 }
 
@@ -816,31 +879,55 @@ int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
     if (start >= S) return RVZ_DONE;
     const int bsz = S - start < B ? S - start : B;
     const int first = e->next_batch == 0;
+    const int ex = e->pending;
+    const float* pol = e->pend_policy;
+    const float* val = e->pend_value;
+    const int lg = e->pend_is_logits;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
     if (e->cfg.leaf_dtype == RVZ_LEAF_F32) {
         float* x = (float*)leaf_x;
-        if (e->BS == 8) hipLaunchKernelGGL((k_select<8, float>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
-        else hipLaunchKernelGGL((k_select<6, float>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
+        if (e->BS == 8) hipLaunchKernelGGL((k_step<8, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
+        else hipLaunchKernelGGL((k_step<6, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
     } else {
         __hip_bfloat16* x = (__hip_bfloat16*)leaf_x;
-        if (e->BS == 8) hipLaunchKernelGGL((k_select<8, __hip_bfloat16>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
-        else hipLaunchKernelGGL((k_select<6, __hip_bfloat16>), grid, block, 0, e->stream, e->v, first, bsz, x, need);
+        if (e->BS == 8) hipLaunchKernelGGL((k_step<8, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
+        else hipLaunchKernelGGL((k_step<6, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
     }
+    e->pending = 0;
     e->next_batch += 1;
     e->counters[0] += 1;
-    return launch_check(e, "k_select");
+    return launch_check(e, "k_step");
 }
 
 int rvz_search_submit(rvz_engine* e, const float* policy, int32_t is_logits, const float* value) {
     if (!e || !policy || !value) return RVZ_EINVAL;
+    if (!e->searching || e->next_batch == 0) {
+        e->err = "rvz_search_submit without a preceding rvz_search_step";
+        return RVZ_EINVAL;
+    }
+    if (e->pending) { e->err = "rvz_search_submit twice for one batch"; return RVZ_EINVAL; }
+    // deferred: the expand + backup runs at the head of the next k_step / k_act launch (or of
+    // k_expand_backup for rvz_search_visits); policy/value must stay valid until then.
+    e->pending = 1;
+    e->pend_policy = policy;
+    e->pend_value = value;
+    e->pend_is_logits = is_logits;
+    return RVZ_OK;
+}
+
+static int flush_pending(rvz_engine* e) {
+    if (!e->pending) return RVZ_OK;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
-    if (e->BS == 8) hipLaunchKernelGGL(k_expand_backup<8>, grid, block, 0, e->stream, e->v, policy, is_logits, value);
-    else hipLaunchKernelGGL(k_expand_backup<6>, grid, block, 0, e->stream, e->v, policy, is_logits, value);
+    if (e->BS == 8) hipLaunchKernelGGL(k_expand_backup<8>, grid, block, 0, e->stream, e->v, e->pend_policy, e->pend_is_logits, e->pend_value);
+    else hipLaunchKernelGGL(k_expand_backup<6>, grid, block, 0, e->stream, e->v, e->pend_policy, e->pend_is_logits, e->pend_value);
+    e->pending = 0;
     return launch_check(e, "k_expand_backup");
 }
 
 int rvz_search_visits(rvz_engine* e, int32_t* out) {
     if (!e || !out) return RVZ_EINVAL;
+    int r = flush_pending(e);
+    if (r != RVZ_OK) return r;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
     if (e->BS == 8) hipLaunchKernelGGL(k_visits<8>, grid, block, 0, e->stream, e->v, out);
     else hipLaunchKernelGGL(k_visits<6>, grid, block, 0, e->stream, e->v, out);
@@ -850,9 +937,11 @@ int rvz_search_visits(rvz_engine* e, int32_t* out) {
 int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, int32_t* out_idx,
             double* out_p) {
     if (!e || !out_idx || !out_p) return RVZ_EINVAL;
+    const int ex = e->pending;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
-    if (e->BS == 8) hipLaunchKernelGGL(k_act<8>, grid, block, 0, e->stream, e->v, temperature, u, apply, out_idx, out_p);
-    else hipLaunchKernelGGL(k_act<6>, grid, block, 0, e->stream, e->v, temperature, u, apply, out_idx, out_p);
+    if (e->BS == 8) hipLaunchKernelGGL(k_act<8>, grid, block, 0, e->stream, e->v, ex, e->pend_policy, e->pend_is_logits, e->pend_value, temperature, u, apply, out_idx, out_p);
+    else hipLaunchKernelGGL(k_act<6>, grid, block, 0, e->stream, e->v, ex, e->pend_policy, e->pend_is_logits, e->pend_value, temperature, u, apply, out_idx, out_p);
+    e->pending = 0;
     if (apply) e->searching = 0;
     return launch_check(e, "k_act");
 }
@@ -867,16 +956,22 @@ int rvz_counters(const rvz_engine* e, int64_t* out2) {
 int rvz_stats_enable(rvz_engine* e, int32_t on) {
     if (!e) return RVZ_EINVAL;
     e->v.stats = on ? e->stats_buf : nullptr;
-    if (on) RVZ_HIP(hipMemsetAsync(e->stats_buf, 0, 4 * sizeof(unsigned long long), e->stream), e);
+    if (on) RVZ_HIP(hipMemsetAsync(e->stats_buf, 0, 3 * (size_t)e->v.G * sizeof(unsigned long long), e->stream), e);
     return RVZ_OK;
 }
 
 int rvz_stats_read(rvz_engine* e, int64_t* out3) {
     if (!e || !out3) return RVZ_EINVAL;
-    unsigned long long h[4] = {0, 0, 0, 0};
-    RVZ_HIP(hipMemcpyAsync(h, e->stats_buf, sizeof(h), hipMemcpyDeviceToHost, e->stream), e);
+    const size_t G = e->v.G;
+    std::vector<unsigned long long> h(3 * G);
+    RVZ_HIP(hipMemcpyAsync(h.data(), e->stats_buf, h.size() * sizeof(unsigned long long),
+                           hipMemcpyDeviceToHost, e->stream), e);
     RVZ_HIP(hipStreamSynchronize(e->stream), e);
-    for (int i = 0; i < 3; ++i) out3[i] = (int64_t)h[i];
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long t = 0;
+        for (size_t g = 0; g < G; ++g) t += h[k * G + g];
+        out3[k] = (int64_t)t;
+    }
     return RVZ_OK;
 }
 
@@ -884,6 +979,8 @@ int rvz_tree_nodes(const rvz_engine* e) { return e ? e->M : RVZ_EINVAL; }
 
 int rvz_tree_export(rvz_engine* e, void* nodes_out, uint32_t* meta_out) {
     if (!e) return RVZ_EINVAL;
+    int r = flush_pending(e);
+    if (r != RVZ_OK) return r;
     const size_t n = (size_t)e->v.G * e->M;
     if (nodes_out) RVZ_HIP(hipMemcpyAsync(nodes_out, e->v.nodes, n * sizeof(Node), hipMemcpyDeviceToDevice, e->stream), e);
     if (meta_out) RVZ_HIP(hipMemcpyAsync(meta_out, e->v.meta, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, e->stream), e);

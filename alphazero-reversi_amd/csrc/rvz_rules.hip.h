@@ -140,4 +140,87 @@ __device__ __forceinline__ bool make_move(GameS& g, int sq) {
     return true;
 }
 
+// ---- wave-cooperative forms: lane l handles direction l & 7, an OR over each 8-lane group -------
+// Every lane ends with the full result. Must be called with all 64 lanes active (DPP).
+__device__ __forceinline__ uint32_t or8_u32(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    return x;
+}
+__device__ __forceinline__ uint64_t or8_u64(uint64_t x) {
+    return ((uint64_t)or8_u32((uint32_t)(x >> 32)) << 32) | or8_u32((uint32_t)x);
+}
+
+// direction d in [0, 8): E, W, S, N, SE, NW, SW, NE as a signed shift (board.py:89-98)
+template <int BS>
+__device__ __forceinline__ int dir_shift(int d) {
+    const int a = d >> 1;
+    const int mag = a == 0 ? 1 : (a == 1 ? BS : (a == 2 ? BS + 1 : BS - 1));
+    return (d & 1) ? -mag : mag;
+}
+
+template <int BS>
+__device__ __forceinline__ uint64_t legal_wave(uint64_t P, uint64_t O, int lane) {
+    const int s = dir_shift<BS>(lane & 7);
+    const int l = s > 0 ? s : 0, r = s > 0 ? 0 : -s;   // (x << l) >> r == sh(x, s)
+    const uint64_t E = ~(P | O) & Geo<BS>::FULL;
+    uint64_t c = ((P << l) >> r) & O;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) c |= ((c << l) >> r) & O;
+    return or8_u64(((c << l) >> r) & E);
+}
+
+template <int BS>
+__device__ __forceinline__ uint64_t flips_wave(int sq, uint64_t P, uint64_t O, int lane) {
+    const int s = dir_shift<BS>(lane & 7);
+    const int l = s > 0 ? s : 0, r = s > 0 ? 0 : -s;
+    const int ad = s > 0 ? s : -s;
+    const uint64_t edge = (ad == 1 || ad == BS - 1) ? Geo<BS>::NOT_COL0
+                          : (ad == BS + 1 ? Geo<BS>::NOT_COLN : ~0ull);
+    uint64_t line = 0, cur = 1ull << sq;
+    for (int k = 0; k < BS - 1; ++k) {
+        cur = (cur << l) >> r;
+        if (!(cur & O & edge)) break;
+        line |= cur;
+    }
+    return or8_u64((cur & P & edge) ? line : 0ull);
+}
+
+// make_move with the wave-cooperative rules; same semantics as make_move<BS>.
+template <int BS>
+__device__ __forceinline__ bool make_move_wave(GameS& g, int sq, int lane) {
+    if (g.over) return false;
+    const int player = g.side;
+    uint64_t P = mine(g), O = theirs(g);
+    if (sq == -1) {
+        if (legal_wave<BS>(P, O, lane)) return false;
+        g.passed += 1;
+        g.side = 3 - player;
+        if (g.passed >= 2) {
+            g.over = 1;
+            set_winner(g);
+        }
+        return true;
+    }
+    if (sq < 0 || sq >= Geo<BS>::NSQ) return false;
+    const uint64_t mb = 1ull << sq;
+    if (!(mb & legal_wave<BS>(P, O, lane))) return false;
+    const uint64_t f = flips_wave<BS>(sq, P, O, lane);
+    P ^= mb | f;
+    O ^= f;
+    if (player == 1) { g.black = P; g.white = O; } else { g.white = P; g.black = O; }
+    g.side = 3 - player;
+    g.passed = 0;
+    if (!legal_wave<BS>(O, P, lane)) {
+        g.side = player;
+        g.passed += 1;
+        if (!legal_wave<BS>(P, O, lane)) {
+            g.over = 1;
+            set_winner(g);
+        }
+    }
+    return true;
+}
+
 }  // namespace rvz

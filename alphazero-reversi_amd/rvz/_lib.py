@@ -60,6 +60,8 @@ SIGNATURES = {
     "rvz_tree_nodes": (C.c_int, [_P]),
     "rvz_tree_export": (C.c_int, [_P, _P, _P]),
     "rvz_footprint": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "rvz_nn_bias_act_f32": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
+    "rvz_nn_bias_act_bf16": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
 }
 
 _lib = None

@@ -76,3 +76,10 @@ def barrier():
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()
+
+
+def aggregate_rate(local_units: float, local_seconds: float) -> Tuple[float, float, float]:
+    """Whole-job throughput: (sum of units over ranks, max seconds over ranks, units/s)."""
+    total = reduce_sum(local_units)
+    dt = reduce_max(local_seconds)
+    return total, dt, total / dt if dt > 0 else float("nan")

@@ -189,6 +189,8 @@ class Engine:
             raise RvzError(f"policy must be [{self.n_games},{self.npol}], value [{self.n_games}]")
         self._stream()
         self._call("rvz_search_submit", ptr(policy), int(bool(is_logits)), ptr(value))
+        # the expand + backup is deferred into the next launch: keep the rows alive until then
+        self._keep = (policy, value)
 
     def search(self, evaluator: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],
                fused_softmax: bool = True):

@@ -109,10 +109,13 @@ class LeafEvaluator:
     rvz expand kernel reads them directly (it fuses the softmax).
     """
 
-    def __init__(self, net: AlphaZeroNetwork, dtype=torch.float32, device=None):
+    def __init__(self, net: AlphaZeroNetwork, dtype=torch.float32, device=None,
+                 fused_epilogue: bool = None):
         net = net.eval()
         dev = torch.device(device) if device is not None else next(net.parameters()).device
         self.dtype, self.device = dtype, dev
+        # on the GPU the conv bias, ReLU and skip add run in one rvz kernel pass (rvz_nn_bias_act)
+        self.fused = dev.type == "cuda" if fused_epilogue is None else bool(fused_epilogue)
         self.board_size = net.board_size
         cl = torch.channels_last
 
@@ -139,9 +142,30 @@ class LeafEvaluator:
             self.vfc1 = fc_nhwc(net.value_fc1, 1)
             self.vfc2 = (net.value_fc2.weight.detach().to(dev, dtype),
                          net.value_fc2.bias.detach().to(dev, dtype))
+            # f32 biases of the trunk convs for the fused epilogue (stem, then conv1/conv2 pairs)
+            trunk = [_fold(net.conv, net.bn)[1]]
+            for b in net.res_blocks:
+                trunk += [_fold(b.conv1, b.bn1)[1], _fold(b.conv2, b.bn2)[1]]
+            self._b32 = [t.to(dev, torch.float32).contiguous() for t in trunk]
+
+    def _bias_act(self, y: torch.Tensor, bias: torch.Tensor, res, relu: bool):
+        from . import _lib
+        cl = torch.channels_last
+        for t in (y, res):
+            if t is not None and not t.is_contiguous(memory_format=cl):
+                raise _lib.RvzError("fused epilogue needs channels_last activations")
+        n_pix = y.shape[0] * y.shape[2] * y.shape[3]
+        fn = (_lib.load().rvz_nn_bias_act_f32 if y.dtype == torch.float32
+              else _lib.load().rvz_nn_bias_act_bf16)
+        _lib.check(fn(y.data_ptr(), bias.data_ptr(), None if res is None else res.data_ptr(),
+                      n_pix, y.shape[1], int(relu), _lib.stream_handle(y.device)),
+                   None, "rvz_nn_bias_act")
+        return y
 
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
+        if self.fused:
+            return self._forward_fused(x)
         cl = torch.channels_last
         h = x.to(self.dtype).contiguous(memory_format=cl)
         w, b = self.stem
@@ -151,6 +175,22 @@ class LeafEvaluator:
             h = F.relu(F.conv2d(y, w2, b2, padding=1) + h)
         n = h.shape[0]
         p = F.relu(F.conv2d(h, *self.pconv))          # [n,2,S,S] channels_last == NHWC memory
+        p = p.permute(0, 2, 3, 1).reshape(n, -1)
+        logits = F.linear(p, *self.pfc)
+        v = F.relu(F.conv2d(h, *self.vconv)).reshape(n, -1)
+        v = torch.tanh(F.linear(F.relu(F.linear(v, *self.vfc1)), *self.vfc2)).squeeze(1)
+        return logits.float(), v.float()
+
+    def _forward_fused(self, x: torch.Tensor):
+        cl = torch.channels_last
+        h = x.to(self.dtype).contiguous(memory_format=cl)
+        w, b = self.stem
+        h = self._bias_act(F.conv2d(h, w, padding=1), self._b32[0], None, True)
+        for i, ((w1, _), (w2, _)) in enumerate(self.blocks):
+            y = self._bias_act(F.conv2d(h, w1, padding=1), self._b32[1 + 2 * i], None, True)
+            h = self._bias_act(F.conv2d(y, w2, padding=1), self._b32[2 + 2 * i], h, True)
+        n = h.shape[0]
+        p = F.relu(F.conv2d(h, *self.pconv))
         p = p.permute(0, 2, 3, 1).reshape(n, -1)
         logits = F.linear(p, *self.pfc)
         v = F.relu(F.conv2d(h, *self.vconv)).reshape(n, -1)

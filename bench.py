@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--instrument-plies", type=int, default=2)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -64,9 +64,11 @@ def make_net(args, device):
 
 
 def instrumented(run, eng, ev, plies):
-    """Eager plies with HIP events around every launch on the launch stream + byte counters."""
+    """Eager plies with HIP events around every launch, on the launch stream, plus the kernels'
+    own algorithmic-byte counters. Each ply is enqueued behind a device-side sleep so the host is
+    ahead of the GPU: event intervals then bracket only the kernel (no host submission gaps)."""
     stream = torch.cuda.current_stream(eng.device)
-    t = {"select": [], "expand_backup": [], "act": [], "nn": []}
+    t = {"step": [], "act": [], "nn": []}
     eng.stats_enable(True)
 
     def timed(key, fn):
@@ -79,18 +81,20 @@ def instrumented(run, eng, ev, plies):
         return r
 
     for _ in range(plies):
+        torch.cuda.synchronize(eng.device)
+        torch.cuda._sleep(int(60e6))        # ~25-30 ms of device time: the host enqueues meanwhile
         eng.search_begin()
-        while timed("select", eng.search_step):
+        while timed("step", eng.search_step):
             logits, value = timed("nn", lambda: ev(eng.leaf_x))
-            timed("expand_backup", lambda: eng.search_submit(logits, value, True))
+            eng.search_submit(logits, value, True)
         timed("act", lambda: eng.act(run.temperature, apply=True))
         run.restart_finished(eng.get_state()[2])
     torch.cuda.synchronize(eng.device)
-    sel, exp, act = eng.stats_read()
+    st, act, _ = eng.stats_read()
     eng.stats_enable(False)
     ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in t.items()}
     n = {k: len(v) for k, v in t.items()}
-    return ms, n, {"select": sel, "expand_backup": exp, "act": act}
+    return ms, n, {"step": st, "act": act}
 
 
 def cpu_baseline(args, net):
@@ -102,7 +106,7 @@ def cpu_baseline(args, net):
     torch.set_num_threads(cores)
     cpu_net = make_net(args, "cpu")
     cpu_net.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
-    G = 64
+    G = 192                                   # ~11 s of C2 work on 16 host threads
     games = [O.new_game(args.board) for _ in range(G)]
     mts = [O.MT(args.seed + g) for g in range(G)]
     srch = O.Search(G, args.sims, args.batch, 1.0, bs=args.board)
@@ -184,19 +188,17 @@ def main():
     rdist.barrier()
     s1 = int(run.steps.item())
     eng.check()
-    dt = rdist.reduce_max(t1 - t0)
-    total = rdist.reduce_sum(s1 - s0)
-    value = total / dt
+    total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
 
     ms, n, bytes_ = instrumented(run, eng, ev, args.instrument_plies)
     eng.check()
     kernels = {}
-    for k in ("select", "expand_backup", "act"):
+    for k in ("step", "act"):
         per_launch = bytes_[k] / max(1, n[k])
         kernels[k] = {"avg_us": ms[k] * 1e3, "launches_per_ply": n[k] // args.instrument_plies,
                       "alg_bytes_per_launch": per_launch,
                       "achieved_GBs": per_launch / (ms[k] * 1e-3) / 1e9}
-    dom = max(("select", "expand_backup", "act"),
+    dom = max(("step", "act"),
               key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
     traffic = None
     if os.path.exists(args.pmc):

@@ -92,7 +92,10 @@ int rvz_search_begin(rvz_engine *e);
 int rvz_search_step(rvz_engine *e, void *leaf_x, int32_t *need);
 /* _process_batch pass 2 (mcts.py:600-623): expand every waiting leaf from policy row g and back
  * up value[g]. policy is [n_games, S*S+1] float32: softmaxed probabilities (is_logits = 0,
- * exactly mcts.py:596's input) or raw logits (is_logits = 1: softmax fused into the kernel). */
+ * exactly mcts.py:596's input) or raw logits (is_logits = 1: softmax fused into the kernel).
+ * Deferred: the work runs at the head of the next rvz_search_step / rvz_act launch (fused into
+ * that kernel) or of rvz_search_visits / rvz_tree_export, so policy and value must stay valid and
+ * unmodified on the stream until that call. */
 int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, const float *value);
 /* {move: child.visit_count} (mcts.py:406-407) as int32 [n_games, S*S+1] */
 int rvz_search_visits(rvz_engine *e, int32_t *out);
@@ -109,8 +112,8 @@ int rvz_act(rvz_engine *e, double temperature, const double *u, int32_t apply, i
 int rvz_counters(const rvz_engine *e, int64_t *out2 /* host */);
 /* Algorithmic-byte counters (bench roofline): while enabled, every search kernel adds the bytes
  * its algorithm must move (nodes scanned, planes/rows written, backups) to a device counter;
- * read returns host int64[3] = {select, expand_backup, act} since the last enable. Off by default
- * (one atomic per game per launch when on). */
+ * read returns host int64[3] = {k_step (expand + select), k_act (expand + act), standalone
+ * k_expand_backup} since the last enable. Off by default (one atomic per game per launch). */
 int rvz_stats_enable(rvz_engine *e, int32_t on);
 int rvz_stats_read(rvz_engine *e, int64_t *out3 /* host */);
 /* Tree export for tests: nodes_out [n_games * nodes_per_game] x {int32 N, f32 W, f32 P, f32 C},
@@ -119,6 +122,16 @@ int rvz_tree_nodes(const rvz_engine *e);
 int rvz_tree_export(rvz_engine *e, void *nodes_out, uint32_t *meta_out);
 /* Sizes of the engine's device-resident state, for DESIGN/bench accounting (host out). */
 int rvz_footprint(const rvz_engine *e, int64_t *bytes_tree, int64_t *bytes_env);
+
+/* ---- leaf-evaluator helpers (the policy/value net, not the reference path) -- */
+/* In place over an NHWC (channels_last) activation of n_pix pixels x channels (conv output with
+ * the BN-folded conv bias not yet added): x = act(x + bias[c] (+ residual)), act = ReLU when
+ * relu != 0 — network.py:23-28,97's bias/BN, skip add and ReLU in one pass. residual may be NULL.
+ * f32: channels % 4 == 0; bf16 (x, residual bf16, bias f32): channels % 8 == 0. */
+int rvz_nn_bias_act_f32(float *x, const float *bias, const float *residual, int64_t n_pix,
+                        int32_t channels, int32_t relu, void *hip_stream);
+int rvz_nn_bias_act_bf16(void *x, const float *bias, const void *residual, int64_t n_pix,
+                         int32_t channels, int32_t relu, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -68,7 +68,7 @@ def test_selfplay_dropin_records(tmp_path):
     import rvz
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 2, 32).cuda()
-    sp = rvz.SelfPlay(net, {"num_simulations": 64, "c_puct": 1.0, "temperature": 1.0,
+    sp = rvz.SelfPlay(net, {"num_simulations": 128, "c_puct": 1.0, "temperature": 1.0,
                             "save_dir": str(tmp_path), "seed": 3})
     games = sp.generate_games(8)
     assert len(games) == 8
