@@ -1,0 +1,70 @@
+"""The leaf evaluator on the GPU: the fused conv epilogue (rvz_nn_bias_act) against PyTorch ops,
+and the whole evaluator against the reference-shaped module (fp32 tolerance; bf16 looser)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("relu", [False, True])
+def test_bias_act_f32_bit_exact(res, relu):
+    from rvz import _lib
+    cl = torch.channels_last
+    torch.manual_seed(1)
+    x = torch.randn(1000, 64, 8, 8, device="cuda").contiguous(memory_format=cl)
+    b = torch.randn(64, device="cuda")
+    r = torch.randn(1000, 64, 8, 8, device="cuda").contiguous(memory_format=cl) if res else None
+    ref = x + b.view(1, -1, 1, 1)
+    if res:
+        ref = ref + r
+    if relu:
+        ref = F.relu(ref)
+    y = x.clone(memory_format=cl)
+    _lib.check(_lib.load().rvz_nn_bias_act_f32(y.data_ptr(), b.data_ptr(),
+                                              r.data_ptr() if res else None, 1000 * 64, 64,
+                                              int(relu), _lib.stream_handle()), None, "bias_act")
+    assert torch.equal(y, ref)
+
+
+def test_bias_act_bf16_close():
+    from rvz import _lib
+    cl = torch.channels_last
+    x = torch.randn(512, 64, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    r = torch.randn(512, 64, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
+    b = torch.randn(64, device="cuda")
+    ref = F.relu(x.float() + b.view(1, -1, 1, 1) + r.float()).to(torch.bfloat16)
+    y = x.clone(memory_format=cl)
+    _lib.check(_lib.load().rvz_nn_bias_act_bf16(y.data_ptr(), b.data_ptr(), r.data_ptr(),
+                                               512 * 64, 64, 1, _lib.stream_handle()), None, "b")
+    assert (y.float() - ref.float()).abs().max().item() <= 2 ** -7 * ref.float().abs().max().item()
+
+
+@pytest.mark.parametrize("blocks,filters", [(6, 64), (2, 32)])
+def test_evaluator_fp32_matches_module(blocks, filters):
+    import rvz
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
+    with torch.no_grad():   # non-trivial BN statistics
+        for m in net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    x = (torch.rand(2048, 3, 8, 8, device="cuda") > 0.6).float()
+    with torch.no_grad():
+        lr, vr = net(x)
+    scale = lr.abs().max().item()
+    for fused in (True, False):
+        ev = rvz.LeafEvaluator(net, fused_epilogue=fused)
+        l, v = ev(x)
+        # fp32 throughout; only the summation order differs (BN folding, NHWC igemm vs NCHW)
+        assert (l - lr).abs().max().item() <= 2e-5 * scale
+        assert (v - vr).abs().max().item() <= 1e-4
+        pr = torch.softmax(lr, 1)
+        assert (torch.softmax(l, 1) - pr).abs().max().item() <= 1e-5
+    evb = rvz.LeafEvaluator(net, dtype=torch.bfloat16)     # throughput mode, not parity grade
+    lb, vb = evb(x)
+    assert (torch.softmax(lb, 1) - torch.softmax(lr, 1)).abs().max().item() < 0.1
+    assert (vb - vr).abs().max().item() < 0.3
