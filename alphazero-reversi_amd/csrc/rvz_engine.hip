@@ -81,6 +81,7 @@ struct View {  // kernel argument: device pointers + sizes
     int32_t* plen;
     uint64_t* leaf_legal;
     uint64_t* root_legal;  // [G] legal mask of the current search's root (its children's squares)
+    uint32_t* leaf_meta;   // [G] meta word of the queued leaf (written by select, read by expand)
     int32_t* nexp;
     double* rng_u;          // [G][RNG_DRAWS]
     int32_t* rng_pos;
@@ -140,9 +141,9 @@ __device__ __forceinline__ int wave_argmax_first(float s, bool valid, int lane) 
 // path_reg: lane i holds the i-th node of the path (root = lane 0). Returns the updated visit
 // count of the root in every lane.
 __device__ __forceinline__ int backup_path(Node* nodes, int path_reg, int plen, float value,
-                                           int copies, int lane) {
-    // order this wave's earlier node stores (UCB caches) before the read-modify-write below
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                                           int copies, int lane, bool order_before) {
+    // order this wave's earlier stores to path nodes (UCB caches) before the read-modify-write
+    if (order_before) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     const int j = plen - 1 - lane;  // lane's path index counted from the root
     const int nid = __shfl(path_reg, j < 0 ? 0 : j);
     int n_after = 0;
@@ -173,72 +174,96 @@ __device__ __forceinline__ float ucb_score(const Node& c, float sqrt_np, int tur
     return q + u;
 }
 
-// expand + backup of the queued leaf: _process_batch pass 2 (mcts.py:600-623) and
-// MCTSNode.expand (:141-161). Returns the root's visit count after the backup (-1: nothing to do).
+// Inputs of the pending expand + backup, all loaded at the head of a launch (no dependent loads:
+// the leaf's meta word is kept in per-game scratch by the select that queued it).
+struct ExpIn {
+    int copies, plen, path_reg, e;
+    uint64_t V;
+    uint32_t lm;
+    float val, prob, xpass;
+};
+
 template <int BS>
-__device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lane,
-                                                   const float* __restrict__ policy,
-                                                   int is_logits, const float* __restrict__ value,
+__device__ __forceinline__ ExpIn expand_load(const View& v, int g, int lane,
+                                             const float* __restrict__ policy,
+                                             const float* __restrict__ value) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    ExpIn x;
+    x.copies = v.pend[g];
+    x.plen = v.plen[g];
+    x.path_reg = v.path[g * PATH_CAP + lane];
+    x.V = v.leaf_legal[g];
+    x.e = v.nexp[g];
+    x.lm = v.leaf_meta[g];
+    x.val = value[g];
+    const float* row = policy + (size_t)g * NPOL;
+    x.prob = lane < NSQ ? row[lane] : 0.0f;
+    x.xpass = row[NSQ];
+    return x;
+}
+
+// expand + backup of the queued leaf: _process_batch pass 2 (mcts.py:600-623) and
+// MCTSNode.expand (:141-161). Returns the root's visit count after the backup (-1: nothing to
+// do) and, when the expanded leaf is the root, its new meta word in *root_meta.
+template <int BS>
+__device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lane, ExpIn x,
+                                                   int is_logits, uint32_t* root_meta,
                                                    unsigned long long& ab) {
     constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
-    const int copies = v.pend[g];
-    if (copies == 0) return -1;
-    const int plen = v.plen[g];
-    const int path_reg = lane < plen ? v.path[g * PATH_CAP + lane] : 0;
-    const uint64_t V = v.leaf_legal[g];
-    const int e = v.nexp[g];
-    const float val = value[g];
-    const float* row = policy + (size_t)g * NPOL;
-    float prob = lane < NSQ ? row[lane] : 0.0f;
-    const float xpass = row[NSQ];
-    const int leaf = __shfl(path_reg, plen - 1);
+    if (x.copies == 0) return -1;
+    const int path_reg = lane < x.plen ? x.path_reg : 0;
+    const int leaf = __shfl(path_reg, x.plen - 1);
     Node* nodes = v.nodes + (size_t)g * v.M;
     uint32_t* meta = v.meta + (size_t)g * v.M;
-    const uint32_t lm = meta[leaf];
+    float prob = x.prob;
     if (is_logits) {  // F.softmax(policy_logits, dim=1) over all S*S+1 outputs (mcts.py:596)
-        const float mx = fmaxf(wave_max_f(lane < NSQ ? prob : -INFINITY), xpass);
+        const float mx = fmaxf(wave_max_f(lane < NSQ ? prob : -INFINITY), x.xpass);
         const float ex = lane < NSQ ? expf(prob - mx) : 0.0f;
-        const float denom = wave_sum_f(ex) + expf(xpass - mx);
+        const float denom = wave_sum_f(ex) + expf(x.xpass - mx);
         prob = ex / denom;
     }
-    const int base = 1 + e * NSQ;
+    const int base = 1 + x.e * NSQ;
     if (base + NSQ > v.M) {
         if (lane == 0) atomicOr(v.err, ERR_POOL);
         return -1;
     }
+    const uint64_t V = x.V;
     if (lane < NSQ && ((V >> lane) & 1ull)) {
         const int idx = __popcll(V & ((1ull << lane) - 1ull));
         Node c;
         c.n = 0; c.w = 0.0f; c.p = prob; c.c = __int_as_float(0x7fc00000);
         nodes[base + idx] = c;
-        meta[base + idx] = meta_pack(lane, 3 - m_turn(lm));
+        meta[base + idx] = meta_pack(lane, 3 - m_turn(x.lm));
     }
+    const uint32_t nlm = x.lm | ((uint32_t)__popcll(V) << 11) | ((uint32_t)x.e << 18);
     if (lane == 0) {
-        meta[leaf] = lm | ((uint32_t)__popcll(V) << 11) | ((uint32_t)e << 18);
-        v.nexp[g] = e + 1;
+        meta[leaf] = nlm;
+        v.nexp[g] = x.e + 1;
         v.pend[g] = 0;
     }
-    const int root_n = backup_path(nodes, path_reg, plen, val, copies, lane);
+    if (leaf == 0 && root_meta) *root_meta = nlm;
+    // the path nodes are not among the nodes written above: no ordering needed before the RMW
+    const int root_n = backup_path(nodes, path_reg, x.plen, x.val, x.copies, lane, false);
     if (v.stats) {
-        // pend/plen/path/legal/nexp reads, policy row + value, leaf meta r/w, children, backup
+        // pend/plen/path/legal/nexp/leaf-meta reads, policy row + value, leaf meta w, children,
+        // backup
         const unsigned long long nch = (unsigned long long)__popcll(V);
-        ab += 8ull + 4ull * plen + 8 + 4 + 4ull * NPOL + 4 + 8 + 20ull * nch + 32ull * plen + 4;
+        ab += 8ull + 4ull * x.plen + 8 + 4 + 4 + 4ull * NPOL + 4 + 4 + 20ull * nch +
+              32ull * x.plen + 8;
     }
     return root_n;
 }
 
 // select: mcts.py:348-386 for one batch of `bsz` traversals + _process_batch pass 1 (:561-585).
-// root_n_known >= 0: the root's visit count is already in registers (fused after a backup).
+// root / root_meta / root_n were loaded (or produced by the expand phase) by the caller.
 template <int BS, typename XT>
 __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int first, int bsz,
-                                             int root_n_known, XT* __restrict__ leaf_x,
-                                             int32_t* __restrict__ need, unsigned long long& ab) {
+                                             const GameS& root, uint32_t root_meta, int root_n,
+                                             XT* __restrict__ leaf_x, int32_t* __restrict__ need,
+                                             unsigned long long& ab) {
     constexpr int NSQ = Geo<BS>::NSQ;
     Node* nodes = v.nodes + (size_t)g * v.M;
     uint32_t* meta = v.meta + (size_t)g * v.M;
-    const GameS root = load_game(v, g);
-    uint32_t root_meta;
-    int root_n;
     if (first) {  // new root (mcts.py:334-341): prior 1.0, turn = side to move
         root_meta = meta_pack(0, root.side);
         root_n = 0;
@@ -252,12 +277,8 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
         const uint64_t rl = root.over ? 0ull : legal_wave<BS>(mine(root), theirs(root), lane);
         if (lane == 0) v.root_legal[g] = rl;
         ab += 20 + 8;
-    } else {
-        root_meta = meta[0];
-        root_n = root_n_known >= 0 ? root_n_known : nodes[0].n;
-        ab += 4 + (root_n_known >= 0 ? 0 : 4);
     }
-    ab += 32;  // game state
+    ab += 32 + 8;  // game state, root meta + N
     int copies = 0, plen = 0, path_reg = 0;
     if (!root.over) {
         int remaining = bsz;
@@ -308,7 +329,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 if (lane == depth) path_reg = node;
             }
             if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
-                root_n = backup_path(nodes, path_reg, depth + 1, m_tv(m), 1, lane);
+                root_n = backup_path(nodes, path_reg, depth + 1, m_tv(m), 1, lane, true);
                 ab += 32ull * (depth + 1);
                 if (--remaining == 0) break;
                 continue;
@@ -320,7 +341,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 const uint32_t code = w == 1 ? 1u : (w == 2 ? 2u : 0u);
                 if (lane == 0) meta[node] = m | (1u << 8) | (code << 9);
                 backup_path(nodes, path_reg, depth + 1, w == 1 ? 1.0f : (w == 2 ? -1.0f : 0.0f),
-                            remaining, lane);
+                            remaining, lane, true);
                 ab += 4 + 32ull * (depth + 1);
                 break;
             }
@@ -335,8 +356,11 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 row[2 * NSQ + lane] = (XT)(float)((V >> lane) & 1ull);
             }
             if (lane < plen) v.path[g * PATH_CAP + lane] = path_reg;
-            if (lane == 0) v.leaf_legal[g] = V;
-            ab += 3ull * NSQ * sizeof(XT) + 4ull * plen + 8;
+            if (lane == 0) {
+                v.leaf_legal[g] = V;
+                v.leaf_meta[g] = m;
+            }
+            ab += 3ull * NSQ * sizeof(XT) + 4ull * plen + 12;
             break;
         }
     }
@@ -349,7 +373,8 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
 }
 
 // One search round: the previous batch's expand + backup (when a submit is pending), then the
-// next batch's selection, in one launch (one wave per game).
+// next batch's selection, in one launch (one wave per game). Every load that does not depend on
+// another is issued at the head.
 template <int BS, typename XT>
 __global__ __launch_bounds__(256) void k_step(View v, int expand, const float* __restrict__ policy,
                                               int is_logits, const float* __restrict__ value,
@@ -358,10 +383,20 @@ __global__ __launch_bounds__(256) void k_step(View v, int expand, const float* _
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (g >= v.G) return;
+    const GameS root = load_game(v, g);
+    uint32_t root_meta = 0;
+    int root_n = 0;
+    if (!first) {
+        root_meta = v.meta[(size_t)g * v.M];
+        root_n = v.nodes[(size_t)g * v.M].n;
+    }
     unsigned long long ab_e = 0, ab_s = 0;
-    int root_n = -1;
-    if (expand) root_n = expand_backup_phase<BS>(v, g, lane, policy, is_logits, value, ab_e);
-    select_phase<BS, XT>(v, g, lane, first, bsz, root_n, leaf_x, need, ab_s);
+    if (expand) {
+        const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
+        const int rn = expand_backup_phase<BS>(v, g, lane, x, is_logits, &root_meta, ab_e);
+        if (rn >= 0) root_n = rn;
+    }
+    select_phase<BS, XT>(v, g, lane, first, bsz, root, root_meta, root_n, leaf_x, need, ab_s);
     if (v.stats && lane == 0) v.stats[g] += ab_s + ab_e;  // per-game slot: no contention
 }
 
@@ -373,7 +408,8 @@ __global__ __launch_bounds__(256) void k_expand_backup(View v, const float* __re
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (g >= v.G) return;
     unsigned long long ab = 0;
-    expand_backup_phase<BS>(v, g, lane, policy, is_logits, value, ab);
+    const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
+    expand_backup_phase<BS>(v, g, lane, x, is_logits, nullptr, ab);
     if (v.stats && lane == 0) v.stats[2 * (size_t)v.G + g] += ab;
 }
 
@@ -428,7 +464,10 @@ __global__ __launch_bounds__(256) void k_act(View v, int expand, const float* __
     const int g = blockIdx.x * WPB + wid;
     if (g >= v.G) return;
     unsigned long long ab = 0;
-    if (expand) expand_backup_phase<BS>(v, g, lane, policy, is_logits, value, ab);
+    if (expand) {
+        const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
+        expand_backup_phase<BS>(v, g, lane, x, is_logits, nullptr, ab);
+    }
     GameS gm = load_game(v, g);
     double* prow = out_p + (size_t)g * NPOL;
     if (gm.over) {
@@ -629,6 +668,11 @@ struct rvz_engine {
     int64_t counters[2] = {0, 0};
     View v;
     unsigned long long* stats_buf = nullptr;
+    // launch timing (rvz_timing_enable): HIP event pairs around k_step / k_act on the stream
+    int timing = 0;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<std::pair<int, size_t>> ev_marks;  // (kind 0 = k_step, 1 = k_act, first event)
     std::vector<void*> allocs;
     std::string err;
 };
@@ -655,6 +699,30 @@ static int launch_check(rvz_engine* e, const char* what) {
 }
 
 static int grid_games(int G) { return (G + WPB - 1) / WPB; }
+
+// Timing events: no system-scope fence (a fenced record writes back and invalidates the caches,
+// which would both slow the timed kernel and inflate the interval).
+static hipEvent_t timing_event(rvz_engine* e) {
+    if (e->ev_used == e->ev_pool.size()) {
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableSystemFence) != hipSuccess) return nullptr;
+        e->ev_pool.push_back(ev);
+    }
+    return e->ev_pool[e->ev_used++];
+}
+
+static void timing_begin(rvz_engine* e, int kind) {
+    if (!e->timing) return;
+    hipEvent_t a = timing_event(e), b = timing_event(e);
+    if (!a || !b) { e->timing = 0; return; }
+    e->ev_marks.push_back({kind, e->ev_used - 2});
+    (void)hipEventRecord(a, e->stream);
+}
+
+static void timing_end(rvz_engine* e) {
+    if (!e->timing || e->ev_marks.empty()) return;
+    (void)hipEventRecord(e->ev_pool[e->ev_marks.back().second + 1], e->stream);
+}
 
 template <typename T>
 static T* dalloc(rvz_engine* e, size_t count) {
@@ -713,6 +781,7 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     v.plen = dalloc<int32_t>(e, G);
     v.leaf_legal = dalloc<uint64_t>(e, G);
     v.root_legal = dalloc<uint64_t>(e, G);
+    v.leaf_meta = dalloc<uint32_t>(e, G);
     v.nexp = dalloc<int32_t>(e, G);
     v.rng_u = dalloc<double>(e, (size_t)G * RNG_DRAWS);
     v.rng_pos = dalloc<int32_t>(e, G);
@@ -726,6 +795,8 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     s = s == hipSuccess ? hipMemset(v.rng_pos, 0, sizeof(int32_t) * G) : s;
     s = s == hipSuccess ? hipMemset(v.meta, 0, sizeof(uint32_t) * (size_t)G * e->M) : s;
     s = s == hipSuccess ? hipMemset(v.root_legal, 0, sizeof(uint64_t) * G) : s;
+    s = s == hipSuccess ? hipMemset(v.leaf_meta, 0, sizeof(uint32_t) * G) : s;
+    s = s == hipSuccess ? hipMemset(v.path, 0, sizeof(int32_t) * G * PATH_CAP) : s;
     if (s == hipSuccess) s = hipDeviceSynchronize();
     if (s != hipSuccess) {
         g_create_error = std::string("device init: ") + hipGetErrorString(s);
@@ -748,6 +819,7 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
 
 void rvz_destroy(rvz_engine* e) {
     if (!e) return;
+    for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     for (void* p : e->allocs)
         if (p) (void)hipFree(p);
     delete e;
@@ -884,6 +956,7 @@ int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
     const float* val = e->pend_value;
     const int lg = e->pend_is_logits;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    timing_begin(e, 0);
     if (e->cfg.leaf_dtype == RVZ_LEAF_F32) {
         float* x = (float*)leaf_x;
         if (e->BS == 8) hipLaunchKernelGGL((k_step<8, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
@@ -893,6 +966,7 @@ int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
         if (e->BS == 8) hipLaunchKernelGGL((k_step<8, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
         else hipLaunchKernelGGL((k_step<6, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
     }
+    timing_end(e);
     e->pending = 0;
     e->next_batch += 1;
     e->counters[0] += 1;
@@ -939,8 +1013,10 @@ int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, i
     if (!e || !out_idx || !out_p) return RVZ_EINVAL;
     const int ex = e->pending;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    timing_begin(e, 1);
     if (e->BS == 8) hipLaunchKernelGGL(k_act<8>, grid, block, 0, e->stream, e->v, ex, e->pend_policy, e->pend_is_logits, e->pend_value, temperature, u, apply, out_idx, out_p);
     else hipLaunchKernelGGL(k_act<6>, grid, block, 0, e->stream, e->v, ex, e->pend_policy, e->pend_is_logits, e->pend_value, temperature, u, apply, out_idx, out_p);
+    timing_end(e);
     e->pending = 0;
     if (apply) e->searching = 0;
     return launch_check(e, "k_act");
@@ -971,6 +1047,32 @@ int rvz_stats_read(rvz_engine* e, int64_t* out3) {
         unsigned long long t = 0;
         for (size_t g = 0; g < G; ++g) t += h[k * G + g];
         out3[k] = (int64_t)t;
+    }
+    return RVZ_OK;
+}
+
+int rvz_timing_enable(rvz_engine* e, int32_t on) {
+    if (!e) return RVZ_EINVAL;
+    e->timing = on ? 1 : 0;
+    e->ev_used = 0;
+    e->ev_marks.clear();
+    return RVZ_OK;
+}
+
+int rvz_timing_read(rvz_engine* e, double* out_ms, int32_t* out_n) {
+    if (!e || !out_ms || !out_n) return RVZ_EINVAL;
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);
+    double sum[2] = {0.0, 0.0};
+    int32_t n[2] = {0, 0};
+    for (const auto& mk : e->ev_marks) {
+        float ms = 0.0f;
+        RVZ_HIP(hipEventElapsedTime(&ms, e->ev_pool[mk.second], e->ev_pool[mk.second + 1]), e);
+        sum[mk.first] += ms;
+        n[mk.first] += 1;
+    }
+    for (int k = 0; k < 2; ++k) {
+        out_ms[k] = n[k] ? sum[k] / n[k] : 0.0;
+        out_n[k] = n[k];
     }
     return RVZ_OK;
 }

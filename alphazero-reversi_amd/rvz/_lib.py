@@ -57,6 +57,8 @@ SIGNATURES = {
     "rvz_counters": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "rvz_stats_enable": (C.c_int, [_P, C.c_int32]),
     "rvz_stats_read": (C.c_int, [_P, C.POINTER(C.c_int64)]),
+    "rvz_timing_enable": (C.c_int, [_P, C.c_int32]),
+    "rvz_timing_read": (C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "rvz_tree_nodes": (C.c_int, [_P]),
     "rvz_tree_export": (C.c_int, [_P, _P, _P]),
     "rvz_footprint": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),

@@ -1,0 +1,254 @@
+"""Batched arena / ELO evaluation (reference src/arena/arena.py:19-389).
+
+``ELORatingSystem`` mirrors arena.py:19-135 (K-factor, expected score, sequential updates,
+leaderboard, JSON save/load). ``ELOPlayer`` and ``Arena`` keep the reference's API
+(``add_player``, ``play_game``, ``run_tournament``, ``print_leaderboard``, ``save_results``), but
+the games of a matchup are played in lockstep on the GPU: one rvz engine per player (its own MCTS
+parameters and evaluator) searches every game each ply, and the move of the player to move is
+applied — the reference's ``current_player.get_move(game)`` (arena.py:244-262) for a whole batch.
+Results are then folded into the ratings in exactly the reference's game order, so the ELO
+history is what the sequential tournament would record for the same game outcomes.
+
+Randomness: each ply draws one ``random_sample()`` per game from a seeded NumPy generator and hands
+it to the mover's act kernel (the reference draws from the global NumPy RNG, game after game);
+random players (model None) pick with ``random.Random`` like ``random.choice`` (arena.py:178-180).
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import time
+from datetime import datetime
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .engine import Engine
+from .network import LeafEvaluator
+
+
+class ELORatingSystem:
+    def __init__(self, k: float = 32, initial_rating: float = 1500.0):
+        self.k = k
+        self.initial_rating = initial_rating
+        self.ratings: Dict[str, float] = {}
+        self.games_played: Dict[str, int] = {}
+        self.history: List[Dict] = []
+
+    def add_player(self, player_id: str, rating: Optional[float] = None):
+        if player_id not in self.ratings:
+            self.ratings[player_id] = self.initial_rating if rating is None else rating
+            self.games_played[player_id] = 0
+
+    def get_rating(self, player_id: str) -> float:
+        return self.ratings.get(player_id, self.initial_rating)
+
+    @staticmethod
+    def get_expected_score(rating_a: float, rating_b: float) -> float:
+        return 1.0 / (1.0 + 10.0 ** ((rating_b - rating_a) / 400.0))
+
+    def update_ratings(self, player_a: str, player_b: str, score_a: float) -> Dict:
+        self.add_player(player_a)
+        self.add_player(player_b)
+        ra, rb = self.ratings[player_a], self.ratings[player_b]
+        ea = self.get_expected_score(ra, rb)
+        eb = 1.0 - ea
+        na = ra + self.k * (score_a - ea)
+        nb = rb + self.k * ((1 - score_a) - eb)
+        self.ratings[player_a], self.ratings[player_b] = na, nb
+        self.games_played[player_a] += 1
+        self.games_played[player_b] += 1
+        rec = {"timestamp": time.time(), "player_a": player_a, "player_b": player_b,
+               "score_a": score_a, "score_b": 1.0 - score_a, "rating_a_before": ra,
+               "rating_b_before": rb, "rating_a_after": na, "rating_b_after": nb}
+        self.history.append(rec)
+        return rec
+
+    def get_leaderboard(self) -> List[Dict]:
+        board = [{"player_id": p, "rating": r, "games_played": self.games_played[p]}
+                 for p, r in self.ratings.items()]
+        return sorted(board, key=lambda x: x["rating"], reverse=True)
+
+    def save_ratings(self, filepath: str):
+        with open(filepath, "w") as f:
+            json.dump({"k": self.k, "initial_rating": self.initial_rating,
+                       "ratings": self.ratings, "games_played": self.games_played,
+                       "history": self.history, "last_updated": datetime.now().isoformat()},
+                      f, indent=2)
+
+    @classmethod
+    def load_ratings(cls, filepath: str) -> "ELORatingSystem":
+        with open(filepath) as f:
+            d = json.load(f)
+        elo = cls(k=d["k"], initial_rating=d["initial_rating"])
+        elo.ratings = {k: float(v) for k, v in d["ratings"].items()}
+        elo.games_played = {k: int(v) for k, v in d["games_played"].items()}
+        elo.history = d.get("history", [])
+        return elo
+
+
+class ELOPlayer:
+    """A model player (MCTS with its own parameters) or, with model None, a random player."""
+
+    def __init__(self, player_id: str, model=None, mcts_params: Optional[Dict] = None,
+                 device: str = "cuda", nn_dtype=torch.float32):
+        self.player_id = player_id
+        self.model = model
+        self.device = torch.device(device)
+        params = mcts_params or {"num_simulations": 800, "c_puct": 1.0, "temperature": 1.0}
+        self.num_simulations = int(params.get("num_simulations", 800))
+        self.c_puct = float(params.get("c_puct", 1.0))
+        self.batch_size = int(params.get("batch_size", 64))
+        self.evaluator = None
+        if model is not None:
+            model.eval()
+            model.to(self.device)
+            self.evaluator = LeafEvaluator(model, dtype=nn_dtype, device=self.device)
+
+    def reset(self):
+        """Searches start from a fresh root every move (mcts.py:334): nothing to reset."""
+
+
+class Arena:
+    def __init__(self, elo_system: Optional[ELORatingSystem] = None, seed: int = 0):
+        self.elo = elo_system if elo_system is not None else ELORatingSystem()
+        self.players: Dict[str, ELOPlayer] = {}
+        self.np_rng = np.random.RandomState(seed)
+        self.py_rng = random.Random(seed)
+
+    def add_player(self, player: ELOPlayer):
+        self.players[player.player_id] = player
+        self.elo.add_player(player.player_id)
+
+    # ------------------------------------------------------------------ batched games
+    def play_games(self, black_ids: Sequence[str], white_ids: Sequence[str]) -> List[float]:
+        """Play len(black_ids) games in lockstep; game g has black_ids[g] (moves first) against
+        white_ids[g]. Returns each game's result for its black player: 1.0 / 0.5 / 0.0
+        (arena.py:264-282). Every player that appears gets one engine over all games."""
+        G = len(black_ids)
+        if G == 0:
+            return []
+        ids = sorted(set(black_ids) | set(white_ids))
+        for pid in ids:
+            if pid not in self.players:
+                raise ValueError(f"One or both players not found: {pid}")
+        dev = next(iter(self.players[p].device for p in ids))
+        engines = {}
+        for pid in ids:
+            pl = self.players[pid]
+            if pl.model is not None:
+                engines[pid] = Engine(G, pl.num_simulations, pl.batch_size, pl.c_puct, device=dev)
+        env = Engine(G, 64, 64, device=dev)          # the authoritative boards (env only)
+        env.reset(range(G))
+        black = np.asarray([ids.index(b) for b in black_ids])
+        white = np.asarray([ids.index(w) for w in white_ids])
+        for _ in range(60):                            # every move places a disc
+            b, w, st = env.get_state()
+            status = st.cpu().numpy()
+            if status[:, 1].all():
+                break
+            side = status[:, 0]
+            mover = np.where(side == 1, black, white)  # index into ids per game
+            u = torch.from_numpy(self.np_rng.random_sample(G))
+            move = np.full(G, -1, np.int64)
+            for k, pid in enumerate(ids):
+                games_k = (mover == k) & (status[:, 1] == 0)
+                if not games_k.any():
+                    continue
+                pl = self.players[pid]
+                if pl.model is None:                   # random player: random.choice(valid)
+                    legal = env.legal().cpu().numpy().view(np.uint64)
+                    for g in np.flatnonzero(games_k):
+                        sq = [s for s in range(64) if (int(legal[g]) >> s) & 1]
+                        move[g] = self.py_rng.choice(sq) if sq else -1
+                    continue
+                eng = engines[pid]
+                eng.set_state(b, w, st)
+                eng.search(pl.evaluator)
+                idx, _ = eng.act(1.0, u=u, apply=False)   # arena.py:183-186 uses T = 1.0
+                idx = idx.cpu().numpy()
+                move[games_k] = np.where(idx[games_k] == 64, -1, idx[games_k])
+            over = status[:, 1] != 0
+            sq = torch.from_numpy(np.where(over, 64, move).astype(np.int32)).to(dev)
+            env.apply(sq)                              # make_move; finished games reject it
+        b, w, st = env.get_state()
+        bb = b.cpu().numpy().view(np.uint64)
+        ww = w.cpu().numpy().view(np.uint64)
+        res = []
+        for g in range(G):
+            nb, nw = bin(int(bb[g])).count("1"), bin(int(ww[g])).count("1")
+            res.append(1.0 if nb > nw else (0.0 if nw > nb else 0.5))
+        return res
+
+    def play_game(self, player1_id: str, player2_id: str, verbose: bool = False,
+                  print_games: bool = False) -> float:
+        """One game, player1 Black (arena.py:218-282)."""
+        r = self.play_games([player1_id], [player2_id])[0]
+        if verbose or print_games:
+            print(f"{player1_id} (Black) vs {player2_id} (White): {r}")
+        return r
+
+    def run_tournament(self, rounds: int = 100, verbose: bool = False,
+                       print_games: bool = False) -> Dict:
+        """Round robin (arena.py:288-389): every pair meets `rounds` times, colours alternating
+        by (i + j + round) % 2; all games of a pair are played in one lockstep batch, then the
+        ratings are updated in the reference's game order."""
+        pids = list(self.players.keys())
+        if len(pids) < 2:
+            raise ValueError("Need at least 2 players for a tournament")
+        results = {"games_played": 0, "matchups": {}, "start_time": time.time(),
+                   "end_time": None, "rounds": []}
+        schedule: List[Tuple[int, str, str]] = []     # (round, black, white) in reference order
+        for i in range(len(pids)):
+            for j in range(i + 1, len(pids)):
+                results["matchups"][f"{pids[i]}_vs_{pids[j]}"] = {
+                    "player1": pids[i], "player2": pids[j], "games_played": 0,
+                    "wins1": 0, "wins2": 0, "draws": 0}
+        for rnd in range(rounds):
+            for i in range(len(pids)):
+                for j in range(i + 1, len(pids)):
+                    p1, p2 = pids[i], pids[j]
+                    if (i + j + rnd) % 2 == 0:
+                        p1, p2 = p2, p1
+                    schedule.append((rnd, p1, p2))
+        outcome = self.play_games([s[1] for s in schedule], [s[2] for s in schedule])
+        for rnd in range(rounds):
+            results["rounds"].append({"round": rnd + 1, "games": []})
+        for (rnd, p1, p2), r in zip(schedule, outcome):
+            e1b, e2b = self.elo.get_rating(p1), self.elo.get_rating(p2)
+            self.elo.update_ratings(p1, p2, r)
+            key = f"{p1}_vs_{p2}" if f"{p1}_vs_{p2}" in results["matchups"] else f"{p2}_vs_{p1}"
+            m = results["matchups"][key]
+            m["games_played"] += 1
+            results["games_played"] += 1
+            # wins1 counts wins of the game's first player, as arena.py:346-351 does
+            if r == 1.0:
+                m["wins1"] += 1
+            elif r == 0.0:
+                m["wins2"] += 1
+            else:
+                m["draws"] += 1
+            results["rounds"][rnd]["games"].append({
+                "player1": p1, "player2": p2, "result": r, "elo1_before": e1b,
+                "elo2_before": e2b, "elo1_after": self.elo.get_rating(p1),
+                "elo2_after": self.elo.get_rating(p2)})
+        if verbose or print_games:
+            self.print_leaderboard()
+        results["end_time"] = time.time()
+        results["duration"] = results["end_time"] - results["start_time"]
+        results["leaderboard"] = self.elo.get_leaderboard()
+        return results
+
+    def print_leaderboard(self):
+        print("\nCurrent Leaderboard:")
+        print("Rank  Player ID               Rating  Games Played")
+        print("----  ---------------------  -------  ------------")
+        for i, p in enumerate(self.elo.get_leaderboard(), 1):
+            print(f"{i:4d}  {p['player_id']:22s}  {p['rating']:7.1f}  {p['games_played']:12d}")
+
+    def save_results(self, filepath: str):
+        self.elo.save_ratings(os.path.splitext(filepath)[0] + "_elo.json")
+        with open(filepath, "w") as f:
+            json.dump(self.elo.get_leaderboard(), f, indent=2)

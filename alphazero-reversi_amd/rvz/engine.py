@@ -116,6 +116,16 @@ class Engine:
         self._call("rvz_stats_read", out)
         return int(out[0]), int(out[1]), int(out[2])
 
+    def timing_enable(self, on: bool = True):
+        self._call("rvz_timing_enable", int(bool(on)))
+
+    def timing_read(self):
+        """Mean ms per launch and launch counts of k_step / k_act since timing_enable."""
+        self._stream()
+        ms, n = (C.c_double * 2)(), (C.c_int32 * 2)()
+        self._call("rvz_timing_read", ms, n)
+        return {"step": (ms[0], n[0]), "act": (ms[1], n[1])}
+
     def tree(self):
         """(nodes int32[G, M, 4] = {N, W, P, C} (W/P/C as float32 bits), meta uint32-as-int32[G, M])."""
         self._stream()

@@ -158,7 +158,15 @@ class SelfPlay:
                           "action_probs": [p[k, g] for k in live],
                           "current_players": players, "values": values, "winner": winner})
         self.games_played += G
+        self._last_run = run
         return games
+
+    def training_tensors(self) -> Dict[str, torch.Tensor]:
+        """The last call's games as device training arrays (rvz.trainer.records_to_training)."""
+        from .trainer import records_to_training
+        run = self._last_run
+        return records_to_training(run.rec_black, run.rec_white, run.rec_side, run.rec_idx,
+                                   run.rec_p, run.post_status, run.eng.board_size)
 
     def generate_games(self, num_games: int) -> List[Dict]:
         t0 = time.time()
@@ -171,12 +179,12 @@ class SelfPlay:
         return games
 
     def generate_training_data(self, num_games: int) -> Optional[Dict[str, np.ndarray]]:
+        """self_play.py:161-219: states (n,3,S,S), action_probs (n,S*S+1), values (n,1), float32,
+        built on the device from the engine's records (games in order, plies in order)."""
         games = self.generate_games(num_games)
-        states = [s for g in games for s in g["states"]]
-        probs = [p for g in games for p in g["action_probs"]]
-        values = [v for g in games for v in g["values"]]
-        if not states:
+        if not any(g["states"] for g in games):
             return None
-        return {"states": np.asarray(states, np.float32),
-                "action_probs": np.asarray(probs, np.float32),
-                "values": np.asarray(values, np.float32).reshape(-1, 1)}
+        t = self.training_tensors()
+        return {"states": t["states"].cpu().numpy(),
+                "action_probs": t["policy_targets"].cpu().numpy(),
+                "values": t["value_targets"].cpu().numpy()}

@@ -64,36 +64,36 @@ def make_net(args, device):
 
 
 def instrumented(run, eng, ev, plies):
-    """Eager plies with HIP events around every launch, on the launch stream, plus the kernels'
-    own algorithmic-byte counters. Each ply is enqueued behind a device-side sleep so the host is
-    ahead of the GPU: event intervals then bracket only the kernel (no host submission gaps)."""
-    stream = torch.cuda.current_stream(eng.device)
-    t = {"step": [], "act": [], "nn": []}
+    """Eager plies with the engine's launch timing on (a HIP event pair, without system fence,
+    around every k_step / k_act on the launch stream) and the kernels' own algorithmic-byte
+    counters. Each ply is enqueued behind a device-side sleep so the host runs ahead of the GPU
+    and the intervals bracket only the kernels. The NN is timed separately (back-to-back calls)."""
     eng.stats_enable(True)
-
-    def timed(key, fn):
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        r = fn()
-        b.record(stream)
-        t[key].append((a, b))
-        return r
-
+    eng.timing_enable(True)
     for _ in range(plies):
         torch.cuda.synchronize(eng.device)
         torch.cuda._sleep(int(60e6))        # ~25-30 ms of device time: the host enqueues meanwhile
         eng.search_begin()
-        while timed("step", eng.search_step):
-            logits, value = timed("nn", lambda: ev(eng.leaf_x))
+        while eng.search_step():
+            logits, value = ev(eng.leaf_x)
             eng.search_submit(logits, value, True)
-        timed("act", lambda: eng.act(run.temperature, apply=True))
+        eng.act(run.temperature, apply=True)
         run.restart_finished(eng.get_state()[2])
-    torch.cuda.synchronize(eng.device)
+    t = eng.timing_read()
+    eng.timing_enable(False)
     st, act, _ = eng.stats_read()
     eng.stats_enable(False)
-    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in t.items()}
-    n = {k: len(v) for k, v in t.items()}
+    # evaluator: 10 back-to-back calls on the same leaf tensor between two events
+    stream = torch.cuda.current_stream(eng.device)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev(eng.leaf_x)
+    a.record(stream)
+    for _ in range(10):
+        ev(eng.leaf_x)
+    b.record(stream)
+    torch.cuda.synchronize(eng.device)
+    ms = {"step": t["step"][0], "act": t["act"][0], "nn": a.elapsed_time(b) / 10}
+    n = {"step": t["step"][1], "act": t["act"][1]}
     return ms, n, {"step": st, "act": act}
 
 

@@ -116,6 +116,12 @@ int rvz_counters(const rvz_engine *e, int64_t *out2 /* host */);
  * k_expand_backup} since the last enable. Off by default (one atomic per game per launch). */
 int rvz_stats_enable(rvz_engine *e, int32_t on);
 int rvz_stats_read(rvz_engine *e, int64_t *out3 /* host */);
+/* Launch timing (bench roofline): while enabled, every k_step (rvz_search_step) and k_act
+ * (rvz_act) launch is bracketed by a pair of HIP events recorded on the engine stream, created with
+ * hipEventDisableSystemFence (no cache write-back/invalidate around the timed kernel). read
+ * synchronises and returns the mean milliseconds and the launch counts {k_step, k_act}. */
+int rvz_timing_enable(rvz_engine *e, int32_t on);
+int rvz_timing_read(rvz_engine *e, double *out_ms /* host [2] */, int32_t *out_n /* host [2] */);
 /* Tree export for tests: nodes_out [n_games * nodes_per_game] x {int32 N, f32 W, f32 P, f32 C},
  * meta_out [n_games * nodes_per_game] uint32 (device). nodes_per_game = rvz_tree_nodes(). */
 int rvz_tree_nodes(const rvz_engine *e);

@@ -229,8 +229,35 @@ def make_net_fixture():
     print(f"net_tiny: {len(sd)} tensors")
 
 
+# ---------------------------------------------------------------------------------- F-elo
+def make_elo_fixture(n_updates: int = 200, seed: int = 11):
+    """arena.py:19-135 ELORatingSystem on a seeded sequence of (a, b, score) updates."""
+    import json
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import types
+    # src.arena imports tqdm at module level; the ELO class itself needs nothing else
+    from src.arena.arena import ELORatingSystem  # type: ignore
+    rng = random.Random(seed)
+    players = ["p0", "p1", "p2", "p3"]
+    elo = ELORatingSystem(k=32, initial_rating=1500.0)
+    seq, after = [], []
+    for _ in range(n_updates):
+        a, b = rng.sample(players, 2)
+        score = rng.choice([0.0, 0.5, 1.0])
+        elo.update_ratings(a, b, score)
+        seq.append([a, b, score])
+        after.append([elo.ratings.get(p, 1500.0) for p in players])
+    json.dump({"players": players, "updates": seq, "ratings_after": after,
+               "leaderboard": elo.get_leaderboard()},
+              open(os.path.join(OUT, "elo_sequence.json"), "w"))
+    print(f"elo_sequence: {n_updates} updates")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["board", "net", "mcts"]
+    which = sys.argv[1:] or ["board", "net", "mcts", "elo"]
+    if "elo" in which:
+        make_elo_fixture()
     if "board" in which:
         make_board_vectors()
     if "net" in which:

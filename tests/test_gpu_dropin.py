@@ -84,9 +84,33 @@ def test_selfplay_dropin_records(tmp_path):
         for p in g["action_probs"]:
             assert p.shape == (65,) and abs(p.sum() - 1.0) < 1e-12
         assert g["states"][0][0].sum() == 2 and g["states"][0][1].sum() == 2
+    # the device-side training arrays == the per-game dicts, concatenated (pipeline.py:179-246)
+    t = sp.training_tensors()
+    st = np.concatenate([np.stack(g["states"]) for g in games])
+    pr = np.concatenate([np.stack(g["action_probs"]) for g in games]).astype(np.float32)
+    va = np.concatenate([np.asarray(g["values"], np.float32) for g in games]).reshape(-1, 1)
+    assert np.array_equal(t["states"].cpu().numpy(), st)
+    assert np.array_equal(t["policy_targets"].cpu().numpy(), pr)
+    assert np.array_equal(t["value_targets"].cpu().numpy(), va)
     data = sp.generate_training_data(4)
     assert data["states"].shape[1:] == (3, 8, 8) and data["values"].shape[1] == 1
-    assert data["action_probs"].shape[1] == 65
+    assert data["action_probs"].shape[1] == 65 and len(data["states"]) == len(data["values"])
+
+
+def test_ddp_trainer_single_gpu_step_on_records():
+    """DDPTrainer (no process group) consumes the engine's records directly and learns."""
+    import rvz
+    from rvz.trainer import DDPTrainer
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 2, 32).cuda()
+    sp = rvz.SelfPlay(net, {"num_simulations": 128, "save_dir": "/tmp/rvz_sp_test", "seed": 9})
+    sp.generate_games(16)
+    data = sp.training_tensors()
+    tr = DDPTrainer(net, batch_size=64)
+    first = tr.train_epoch(data, seed=0)
+    for _ in range(4):
+        last = tr.train_epoch(data, seed=1)
+    assert first["steps"] >= 10 and last["train/loss"] < first["train/loss"]
 
 
 def test_selfplay_runner_graph_replay_equals_eager():
