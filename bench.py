@@ -36,17 +36,27 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense peaks, same source
 
 
+PRESETS = {   # BASELINE.json configs (index 0 is the reference's own single CPU game)
+    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8),
+    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8),
+    "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8),   # per GPU, x8 GPUs
+    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=sorted(PRESETS), default="c2",
+                    help="BASELINE.json workload preset; explicit flags override it")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--games", type=int, default=4096, help="games per GPU")
-    ap.add_argument("--sims", type=int, default=800)
+    ap.add_argument("--games", type=int, default=None, help="games per GPU")
+    ap.add_argument("--sims", type=int, default=None)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--blocks", type=int, default=6)
-    ap.add_argument("--filters", type=int, default=64)
-    ap.add_argument("--board", type=int, default=8)
+    ap.add_argument("--blocks", type=int, default=None)
+    ap.add_argument("--filters", type=int, default=None)
+    ap.add_argument("--board", type=int, default=None)
     ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--instrument-plies", type=int, default=2)
@@ -54,7 +64,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    args = ap.parse_args()
+    for k, v in PRESETS[args.config].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    return args
 
 
 def make_net(args, device):
@@ -201,7 +215,7 @@ def main():
     dom = max(("step", "act"),
               key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
     traffic = None
-    if os.path.exists(args.pmc):
+    if os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096:
         try:
             traffic = json.load(open(args.pmc)).get(dom, {}).get("hbm_bytes_per_launch")
         except Exception:
@@ -216,13 +230,14 @@ def main():
     if rank == 0:
         ach = kernels[dom]["achieved_GBs"]
         out = {
-            "metric": "self-play board-steps/sec @ 800 sims/move, 8x8 Reversi",
+            "metric": f"self-play board-steps/sec @ {args.sims} sims/move, "
+                      f"{args.board}x{args.board} Reversi",
             "value": round(value, 2), "unit": "board-steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u64+f32", "data": "synthetic (start position, per-game seeds, random-init net)",
-            "config": {"workload": f"configs[1]: {args.games} games/GPU x {args.sims} sims, "
+            "config": {"workload": f"{args.config}: {args.games} games/GPU x {args.sims} sims, "
                                    f"{args.blocks}x{args.filters} ResNet, {args.board}x{args.board}",
                        "games_per_gpu": args.games, "global_games": args.games * world,
                        "sims": args.sims, "batch": args.batch,

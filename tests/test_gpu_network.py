@@ -66,5 +66,7 @@ def test_evaluator_fp32_matches_module(blocks, filters):
         assert (torch.softmax(l, 1) - pr).abs().max().item() <= 1e-4
     evb = rvz.LeafEvaluator(net, dtype=torch.bfloat16)     # throughput mode, not parity grade
     lb, vb = evb(x)
-    assert (torch.softmax(lb, 1) - torch.softmax(lr, 1)).abs().max().item() < 0.1
-    assert (vb - vr).abs().max().item() < 0.3
+    # bf16 activations: ~3 significant digits on logits of a deep random-init net
+    assert (lb - lr).abs().max().item() <= 0.05 * scale
+    assert (lb.argmax(1) == lr.argmax(1)).float().mean().item() > 0.8
+    assert (vb - vr).abs().max().item() < 0.5
