@@ -101,6 +101,45 @@ def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d):
     return w.detach(), b.detach()
 
 
+def pack_resnet_params(net: AlphaZeroNetwork) -> torch.Tensor:
+    """BN-folded fp32 parameters in the layout of csrc/rvz_resnet.hip (rvz_resnet_fwd_f32)."""
+    F = net.num_filters
+    parts = []
+
+    def put(t):
+        parts.append(t.detach().float().reshape(-1))
+
+    w, b = _fold(net.conv, net.bn)                         # [F,3,3,3] -> [F][tap*3 + ch]
+    put(w.permute(0, 2, 3, 1).reshape(F, 27))
+    put(b)
+    n = sum(x.numel() for x in parts)
+    if n % 4:
+        parts.append(torch.zeros(4 - n % 4, device=w.device))
+    ws, bs = [], []
+    for blk in net.res_blocks:
+        for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
+            w, b = _fold(conv, bn)                         # [n][k][3][3] -> [tap][n][k]
+            ws.append(w.permute(2, 3, 0, 1).reshape(9, F, F))
+            bs.append(b)
+    for t in ws:
+        put(t)
+    for t in bs:
+        put(t)
+    w, b = _fold(net.policy_conv, net.policy_bn)
+    put(w.reshape(2, F))
+    put(b)
+    put(net.policy_fc.weight)
+    put(net.policy_fc.bias)
+    w, b = _fold(net.value_conv, net.value_bn)
+    put(w.reshape(F))
+    put(b)
+    put(net.value_fc1.weight)
+    put(net.value_fc1.bias)
+    put(net.value_fc2.weight.reshape(-1))
+    put(net.value_fc2.bias)
+    return torch.cat(parts).contiguous()
+
+
 class LeafEvaluator:
     """Inference-only evaluator over a fixed leaf batch: (logits f32 [n,S*S+1], value f32 [n]).
 
@@ -110,10 +149,26 @@ class LeafEvaluator:
     """
 
     def __init__(self, net: AlphaZeroNetwork, dtype=torch.float32, device=None,
-                 fused_epilogue: bool = None):
+                 fused_epilogue: bool = None, kernel: str = "auto"):
         net = net.eval()
         dev = torch.device(device) if device is not None else next(net.parameters()).device
         self.dtype, self.device = dtype, dev
+        # kernel: "resnet" = the whole forward in rvz_resnet_fwd_f32 (fp32, 8x8, 64/128 filters),
+        # "miopen" = PyTorch convs (+ the fused epilogue), "auto" = resnet where it applies
+        self.n_blocks, self.filters = len(net.res_blocks), net.num_filters
+        resnet_ok = (dev.type == "cuda" and dtype == torch.float32 and net.board_size == 8
+                     and net.num_filters in (64, 128))
+        if kernel == "resnet" and not resnet_ok:
+            raise ValueError("the fused resnet kernel needs fp32, 8x8, 64 or 128 filters, a GPU")
+        self.use_resnet = kernel == "resnet" or (kernel == "auto" and resnet_ok)
+        self._outs = {}
+        if self.use_resnet:
+            from . import _lib
+            with torch.no_grad():
+                self.params = pack_resnet_params(net).to(dev).contiguous()
+            want = _lib.load().rvz_resnet_params_size(self.filters, self.n_blocks)
+            if want != self.params.numel():
+                raise _lib.RvzError(f"packed params {self.params.numel()} != layout {want}")
         # on the GPU the conv bias, ReLU and skip add run in one rvz kernel pass (rvz_nn_bias_act)
         self.fused = dev.type == "cuda" if fused_epilogue is None else bool(fused_epilogue)
         self.board_size = net.board_size
@@ -162,8 +217,26 @@ class LeafEvaluator:
                    None, "rvz_nn_bias_act")
         return y
 
+    def _forward_resnet(self, x: torch.Tensor):
+        from . import _lib
+        n = x.shape[0]
+        x = x.float().contiguous()
+        outs = self._outs.get(n)
+        if outs is None:   # fixed per batch size: stable addresses under HIP-graph capture
+            outs = (torch.empty(n, self.board_size ** 2 + 1, device=self.device),
+                    torch.empty(n, device=self.device))
+            self._outs[n] = outs
+        logits, value = outs
+        _lib.check(_lib.load().rvz_resnet_fwd_f32(
+            x.data_ptr(), n, self.params.data_ptr(), self.filters, self.n_blocks,
+            logits.data_ptr(), value.data_ptr(), _lib.stream_handle(x.device)),
+            None, "rvz_resnet_fwd_f32")
+        return logits, value
+
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
+        if self.use_resnet:
+            return self._forward_resnet(x)
         if self.fused:
             return self._forward_fused(x)
         cl = torch.channels_last

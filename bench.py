@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--board", type=int, default=None)
     ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--nn-kernel", choices=["auto", "resnet", "miopen"], default="auto",
+                    help="leaf evaluator: rvz_resnet_fwd_f32 (fused fp32 MFMA) or MIOpen convs")
     ap.add_argument("--instrument-plies", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -175,7 +177,7 @@ def main():
     nn_dtype = torch.float32 if args.nn_dtype == "fp32" else torch.bfloat16
 
     net = make_net(args, device)
-    ev = rvz.LeafEvaluator(net, dtype=nn_dtype, device=device)
+    ev = rvz.LeafEvaluator(net, dtype=nn_dtype, device=device, kernel=args.nn_kernel)
     eng = rvz.Engine(args.games, args.sims, args.batch, 1.0, board_size=args.board, device=device,
                      leaf_dtype=torch.float32 if nn_dtype == torch.float32 else torch.bfloat16)
     first_game = rank * args.games          # global game index space: rank r owns a shard
@@ -242,6 +244,7 @@ def main():
                        "games_per_gpu": args.games, "global_games": args.games * world,
                        "sims": args.sims, "batch": args.batch,
                        "nn": f"{args.blocks}x{args.filters}", "nn_dtype": args.nn_dtype,
+                       "nn_kernel": "rvz_resnet_fwd_f32" if ev.use_resnet else "miopen+rvz_nn_bias_act",
                        "graph": not args.no_graph, "parallelism": f"games sharded x{world}"},
             "roofline": {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(ach, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -139,6 +139,16 @@ int rvz_nn_bias_act_f32(float *x, const float *bias, const float *residual, int6
 int rvz_nn_bias_act_bf16(void *x, const float *bias, const void *residual, int64_t n_pix,
                          int32_t channels, int32_t relu, void *hip_stream);
 
+/* The whole policy/value network forward (network.py:30-117, BN folded) in one kernel: x float32
+ * [n, 3, 8, 8] (the leaf planes) -> logits float32 [n, 65], value float32 [n]. fp32 on the
+ * f32-input MFMA, activations resident in LDS. filters 64 (2 boards per workgroup) or 128
+ * (1 board per workgroup), any block count. params: the packed fp32 buffer laid out as in
+ * csrc/rvz_resnet.hip (rvz.network.pack_resnet_params), 16-byte aligned, of
+ * rvz_resnet_params_size(filters, blocks) floats (negative: unsupported shape). */
+int64_t rvz_resnet_params_size(int32_t filters, int32_t blocks);
+int rvz_resnet_fwd_f32(const float *x, int32_t n, const float *params, int32_t filters,
+                       int32_t blocks, float *logits, float *value, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

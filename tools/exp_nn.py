@@ -47,23 +47,28 @@ def graph_time(fn, x, iters=20):
     return a.elapsed_time(b) / iters
 
 
-torch.manual_seed(0)
-net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
-x = (torch.rand(4096, 3, 8, 8, device="cuda") > 0.6).float()
-res = {}
-for bench_mode in (False, True):
-    torch.backends.cudnn.benchmark = bench_mode
-    for dtype in (torch.float32, torch.bfloat16):
-        ev = rvz.LeafEvaluator(net, dtype=dtype)
-        key = f"nhwc_{'fp32' if dtype == torch.float32 else 'bf16'}_bench{int(bench_mode)}"
-        res[key] = round(graph_time(ev, x), 4)
-    with torch.no_grad():
-        res[f"module_nchw_fp32_bench{int(bench_mode)}"] = round(graph_time(lambda t: net(t), x), 4)
+def main():
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
+    x = (torch.rand(4096, 3, 8, 8, device="cuda") > 0.6).float()
+    res = {}
+    for bench_mode in (False, True):
+        torch.backends.cudnn.benchmark = bench_mode
+        for dtype in (torch.float32, torch.bfloat16):
+            ev = rvz.LeafEvaluator(net, dtype=dtype)
+            key = f"nhwc_{'fp32' if dtype == torch.float32 else 'bf16'}_bench{int(bench_mode)}"
+            res[key] = round(graph_time(ev, x), 4)
+        with torch.no_grad():
+            res[f"module_nchw_fp32_bench{int(bench_mode)}"] = round(graph_time(lambda t: net(t), x), 4)
 
-    # conv-only cost of the 12 residual convs (NHWC fp32, no bias)
-    w = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
-    h = torch.randn(4096, 64, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last)
-    res[f"conv3x3_nhwc_fp32_nobias_bench{int(bench_mode)}_ms"] = round(graph_time(lambda t: F.conv2d(t, w, padding=1), h), 4)
-    wn, hn = w.contiguous(), h.contiguous()
-    res[f"conv3x3_nchw_fp32_nobias_bench{int(bench_mode)}_ms"] = round(graph_time(lambda t: F.conv2d(t, wn, padding=1), hn), 4)
-print(json.dumps(res))
+        # conv-only cost of the 12 residual convs (NHWC fp32, no bias)
+        w = torch.randn(64, 64, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+        h = torch.randn(4096, 64, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last)
+        res[f"conv3x3_nhwc_fp32_nobias_bench{int(bench_mode)}_ms"] = round(graph_time(lambda t: F.conv2d(t, w, padding=1), h), 4)
+        wn, hn = w.contiguous(), h.contiguous()
+        res[f"conv3x3_nchw_fp32_nobias_bench{int(bench_mode)}_ms"] = round(graph_time(lambda t: F.conv2d(t, wn, padding=1), hn), 4)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
