@@ -1,5 +1,5 @@
 // rvz_resnet.hip — the whole policy/value ResNet forward of the reference (network.py:30-117) in
-// ONE gfx950 kernel per leaf batch, fp32 end to end on the f32-input MFMA (v_mfma_f32_16x16x4_f32,
+// ONE gfx950 kernel per leaf batch, fp32 end to end on the f32-input MFMA (v_mfma_f32_32x32x2_f32,
 // exact f32 FMA chains; the reference's precision).
 //
 // Why: with MIOpen, every conv layer is a separate launch plus a zero-fill of its output and a
@@ -8,12 +8,15 @@
 // logits/value out; weights stream from L2 (shared by every workgroup).
 //
 // Layout (one workgroup = 4 waves = NBOARD boards; F filters; 8x8 boards):
-//   LDS act[2][NBOARD][10x10 padded pixels][F + 4 floats]   (ping-pong h / y, zero halo)
-//   conv layer = GEMM  M = NBOARD*64 pixels, N = F, K = 9 taps x F channels.
-//   MFMA 16x16x4: A lane l = (pixel l&15 of the M-tile, k-slot l>>4), B lane l = (k-slot l>>4,
-//   channel l&15 of the N-tile). k-slot q of step s of tap t is input channel q*(F/4)+s, so one
-//   ds_read_b128 (A) / global_load_dwordx4 (B) feeds 4 consecutive steps.
-//   Wave w owns N-tiles {w, w+4, ..} and every M-tile: MT*NT = 8 accumulators of 4 floats.
+//   LDS act[2][NBOARD][64 pixels][F + 4 floats]   (ping-pong h / y; no halo: taps that leave the
+//   board are masked to 0). A pixel row is F + 4 floats, so consecutive pixels start 4 banks apart.
+//   conv layer = GEMM  M = NBOARD*64 pixels, N = F, K = 9 taps x F channels, on
+//   v_mfma_f32_32x32x2_f32: A lane l = (pixel l&31 of a 32-pixel M-tile, k-slot l>>5), B lane l =
+//   (k-slot l>>5, channel l&31 of the N-tile); k-slot h of step s is input channel h*(F/2)+s, so
+//   one ds_read_b128 (A) / global_load_dwordx4 (B) feeds 4 steps. Every 16-lane group of a
+//   ds_read_b128 then reads 16 distinct consecutive pixels: bank-conflict free (a 16x16x4 layout
+//   mixed k-slots inside a group: 61% of its LDS cycles were conflicts, rocprof SQ_LDS_BANK_CONFLICT).
+//   Wave w: N-tile, 2 M-tiles -> 2 accumulators of 16 floats.
 // Packed parameter buffer (fp32, BN folded by rvz.LeafEvaluator; offsets in rvz_resnet_layout):
 //   stem_w[F][27] (k = tap*3 + ch), stem_b[F], res_w[2NB][9][F(n)][F(k)], res_b[2NB][F],
 //   pol_w[2][F], pol_b[2], pfc_w[65][128] (in = c*64 + px), pfc_b[65], val_w[F], val_b[1],
@@ -58,26 +61,20 @@ __host__ __device__ inline Layout make_layout(int F, int NB) {
 template <int F, int NBOARD>
 struct Cfg {
     static constexpr int CS = F + 4;                 // padded channel stride (bank spread)
-    static constexpr int BOARD = 100 * CS;           // floats per board per buffer
+    static constexpr int BOARD = 64 * CS;            // floats per board per buffer
     static constexpr int ACT = NBOARD * BOARD;       // floats per buffer
-    static constexpr int XIN = NBOARD * 100 * 4;     // stem input, 3 planes padded to 4
+    static constexpr int XIN = NBOARD * 100 * 4;     // stem input, 3 planes padded to 4 (halo)
     static constexpr int HP = NBOARD * 128;          // policy conv output (NCHW flatten)
     static constexpr int HV = NBOARD * 64;           // value conv output
     static constexpr int H1 = NBOARD * 256;          // value fc1 output
     static constexpr int SMEM = 2 * ACT + XIN + HP + HV + H1;
-    static constexpr int MT = 4 * NBOARD;            // 16-pixel M-tiles (2 board rows each)
-    static constexpr int NT = F / 64;                // N-tiles per wave
-    static_assert(MT * NT == 8, "8 accumulators per wave");
+    static constexpr int MTILES = 2 * NBOARD;        // 32-pixel M-tiles (4 board rows each)
+    static constexpr int NTILES = F / 32;            // 32-channel N-tiles
+    static_assert(MTILES * NTILES == 8, "8 tiles = 4 waves x 2 accumulators");
     static_assert(SMEM * 4 <= 160 * 1024, "fits the 160 KiB LDS of a CU");
 };
 
-// padded pixel index of M-tile row p (0..15) of tile mt, shifted by tap t
-__device__ __forceinline__ int tile_pix(int mt, int p, int t) {
-    const int b = mt >> 2, tr = mt & 3;
-    const int r = 2 * tr + (p >> 3), c = p & 7;
-    const int dr = t / 3 - 1, dc = t % 3 - 1;
-    return b * 100 + (r + 1 + dr) * 10 + (c + 1 + dc);
-}
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // One 3x3 conv layer: out = relu(conv(in) + bias (+ res)), all in LDS.
 template <int F, int NBOARD, bool RES>
@@ -85,71 +82,55 @@ __device__ __forceinline__ void conv_layer(const float* __restrict__ in, float* 
                                            const float* __restrict__ w,   // [9][F][F]
                                            const float* __restrict__ bias, int wave, int lane) {
     using C = Cfg<F, NBOARD>;
-    constexpr int MT = C::MT, NT = C::NT, KQ = F / 4;   // steps per tap
-    const int q = lane >> 4, p = lane & 15;
-    f32x4 acc[MT][NT];
+    constexpr int KH = F / 2;                     // steps per tap (2 k-slots)
+    // wave -> (N-tile, first M-tile): F=64: 2 N-tiles x 4 M-tiles; F=128: 4 N-tiles x 2 M-tiles
+    const int nt = F == 64 ? (wave & 1) : wave;
+    const int mt0 = F == 64 ? 2 * (wave >> 1) : 0;
+    const int h = lane >> 5, m = lane & 31;
+    f32x16 acc0 = {}, acc1 = {};
+    // A: pixel (mt*32 + m) of the workgroup; B: channel nt*32 + m
+    const int pix0 = mt0 * 32 + m, pix1 = pix0 + 32;
+    const int r0 = (pix0 & 63) >> 3, c0 = pix0 & 7, r1 = (pix1 & 63) >> 3, c1 = pix1 & 7;
+    const float* brow = w + (size_t)(nt * 32 + m) * F + h * KH;
+    const int koff = h * KH;
+    for (int t = 0; t < 9; ++t) {
+        const int dr = t / 3 - 1, dc = t % 3 - 1;
+        const bool v0 = (unsigned)(r0 + dr) < 8u && (unsigned)(c0 + dc) < 8u;
+        const bool v1 = (unsigned)(r1 + dr) < 8u && (unsigned)(c1 + dc) < 8u;
+        // out-of-board taps read their own pixel and are zeroed (no halo in LDS)
+        const float* a0p = in + (size_t)(v0 ? pix0 + dr * 8 + dc : pix0) * C::CS + koff;
+        const float* a1p = in + (size_t)(v1 ? pix1 + dr * 8 + dc : pix1) * C::CS + koff;
+        const float* bp = brow + (size_t)t * F * F;
+#pragma unroll 4
+        for (int g = 0; g < KH; g += 4) {
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(bp + g);
+            f32x4 a0 = *reinterpret_cast<const f32x4*>(a0p + g);
+            f32x4 a1 = *reinterpret_cast<const f32x4*>(a1p + g);
+            if (!v0) a0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            if (!v1) a1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // per-lane base addresses: A at (pixel, channel q*KQ), B at (channel n, k q*KQ)
-    int abase[MT];
-#pragma unroll
-    for (int i = 0; i < MT; ++i) abase[i] = tile_pix(i, p, 4) * C::CS + q * KQ;   // tap 4 = center
-    const float* bbase[NT];
-#pragma unroll
-    for (int j = 0; j < NT; ++j) bbase[j] = w + (size_t)((wave + 4 * j) * 16 + p) * F + q * KQ;
-    // K loop over 9 taps x KQ/4 groups of 4 steps, software-pipelined one group deep: the next
-    // group's weight (global/L2) and activation (LDS) operands load under this group's MFMAs.
-    constexpr int GPT = KQ / 4;          // groups per tap
-    constexpr int NG = 9 * GPT;
-    f32x4 a_cur[MT], b_cur[NT], a_nxt[MT], b_nxt[NT];
-    auto load = [&](int it, f32x4* av, f32x4* bv) {
-        const int t = it / GPT, g = (it % GPT) * 4;
-        const int shift = ((t / 3 - 1) * 10 + (t % 3 - 1)) * C::CS;   // tap offset in LDS
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-            bv[j] = *reinterpret_cast<const f32x4*>(bbase[j] + (size_t)t * F * F + g);
-#pragma unroll
-        for (int i = 0; i < MT; ++i)
-            av[i] = *reinterpret_cast<const f32x4*>(in + abase[i] + shift + g);
-    };
-    load(0, a_cur, b_cur);
-    for (int it = 0; it < NG; ++it) {
-        if (it + 1 < NG) load(it + 1, a_nxt, b_nxt);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < NT; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[i][s], b_cur[j][s],
-                                                                    acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) a_cur[i] = a_nxt[i];
-#pragma unroll
-        for (int j = 0; j < NT; ++j) b_cur[j] = b_nxt[j];
-    }
-    // epilogue: D row = (lane>>4)*4 + r (pixel in the tile), col = lane&15 (channel in the tile)
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-        const int n = (wave + 4 * j) * 16 + p;
-        const float bn = bias[n];
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int off = tile_pix(i, 4 * q + r, 4) * C::CS + n;
-                float v = acc[i][j][r] + bn;
-                if (RES) v += out[off];          // skip input h, read then overwritten in place
-                out[off] = fmaxf(v, 0.0f);
+            for (int s = 0; s < 4; ++s) {
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], bv[s], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], bv[s], acc1, 0, 0, 0);
             }
         }
+    }
+    // epilogue: D col = lane&31 (channel), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (pixel)
+    const int n = nt * 32 + m;
+    const float bn = bias[n];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int o0 = (mt0 * 32 + row) * C::CS + n, o1 = o0 + 32 * C::CS;
+        float x0 = acc0[reg] + bn, x1 = acc1[reg] + bn;
+        if (RES) { x0 += out[o0]; x1 += out[o1]; }   // skip input h, read then overwritten in place
+        out[o0] = fmaxf(x0, 0.0f);
+        out[o1] = fmaxf(x1, 0.0f);
     }
 }
 
 template <int F, int NBOARD>
-__global__ __launch_bounds__(256, 1) void k_resnet_fwd(const float* __restrict__ x, int n_boards,
+__global__ __launch_bounds__(256, 2) void k_resnet_fwd(const float* __restrict__ x, int n_boards,
                                                        const float* __restrict__ prm, Layout L,
                                                        int n_blocks, float* __restrict__ logits,
                                                        float* __restrict__ value) {
@@ -164,14 +145,7 @@ __global__ __launch_bounds__(256, 1) void k_resnet_fwd(const float* __restrict__
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g0 = blockIdx.x * NBOARD;
 
-    // zero both activation buffers' halos and the stem input (interior rewritten below)
-    for (int i = tid; i < 2 * NBOARD * 100; i += 256) {
-        const int px = i % 100, r = px / 10, c = px % 10;
-        if (r == 0 || r == 9 || c == 0 || c == 9) {
-            float* dst = smem + (size_t)(i / 100) * 100 * C::CS + (size_t)px * C::CS;
-            for (int k = 0; k < F; k += 4) *reinterpret_cast<float4*>(dst + k) = make_float4(0, 0, 0, 0);
-        }
-    }
+    // zero the stem input (its halo stays 0; the interior is written below)
     for (int i = tid; i < NBOARD * 100 * 4; i += 256) xin[i] = 0.0f;
     __syncthreads();
     for (int i = tid; i < NBOARD * 192; i += 256) {       // x[g][ch][r][c] -> xin[b][pad px][ch]
@@ -198,7 +172,7 @@ __global__ __launch_bounds__(256, 1) void k_resnet_fwd(const float* __restrict__
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) acc = fmaf(src[ch], wv[t * 3 + ch], acc);
             }
-            actA[(b * 100 + (r + 1) * 10 + c + 1) * C::CS + n] = fmaxf(acc + bn, 0.0f);
+            actA[(b * 64 + px) * C::CS + n] = fmaxf(acc + bn, 0.0f);
         }
     }
     __syncthreads();
@@ -217,7 +191,7 @@ __global__ __launch_bounds__(256, 1) void k_resnet_fwd(const float* __restrict__
     for (int o = tid; o < NBOARD * 192; o += 256) {
         const int b = o / 192, rem = o % 192;
         const int c2 = rem / 64, px = rem % 64;            // c2 0,1: policy planes; 2: value
-        const float* a = actA + (b * 100 + (px / 8 + 1) * 10 + px % 8 + 1) * C::CS;
+        const float* a = actA + (b * 64 + px) * C::CS;
         const float* wr = c2 < 2 ? prm + L.pol_w + c2 * F : prm + L.val_w;
         float acc = 0.0f;
         for (int k = 0; k < F; ++k) acc = fmaf(a[k], wr[k], acc);

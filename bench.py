@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL) for real multi-GPU runs; gloo to rehearse several ranks "
+                         "on one device")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     args = ap.parse_args()
     for k, v in PRESETS[args.config].items():
@@ -169,10 +172,11 @@ def main():
     from rvz import dist as rdist
 
     rank, local_rank, world = rdist.env_rank_world()
+    dev_index = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        rdist.init("nccl")
-    device = torch.device("cuda", local_rank if world > 1 else torch.cuda.current_device())
+        torch.cuda.set_device(dev_index)
+        rdist.init(args.dist_backend)
+    device = torch.device("cuda", dev_index if world > 1 else torch.cuda.current_device())
     torch.cuda.set_device(device)
     nn_dtype = torch.float32 if args.nn_dtype == "fp32" else torch.bfloat16
 
