@@ -1,13 +1,24 @@
 // rvz_resnet.hip — the whole policy/value ResNet forward of the reference (network.py:30-117) in
-// ONE gfx950 kernel per leaf batch, fp32 end to end on the f32-input MFMA (v_mfma_f32_32x32x2_f32,
-// exact f32 FMA chains; the reference's precision).
+// ONE gfx950 kernel per leaf batch, in two fp32-class numerics:
 //
-// Why: with MIOpen, every conv layer is a separate launch plus a zero-fill of its output and a
-// bias/skip/ReLU pass, and every activation makes an HBM round trip. Here a workgroup keeps its
-// boards' activations in LDS for the whole network: HBM traffic is the leaf planes in and the
-// logits/value out; weights stream from L2 (shared by every workgroup).
+//  * k_resnet_fwd (rvz_resnet_fwd_f32): the f32-input MFMA v_mfma_f32_32x32x2_f32 — bit-for-bit
+//    k-ordered fp32 FMA chains, the reference's precision, at the f32 matrix rate (157 TF/s).
+//  * k_resnet_split (rvz_resnet_fwd_split): every fp32 operand split exactly into three bf16
+//    parts, x = x0 + (x1 + x2) (8 significant bits each, 24 together), and the conv GEMMs run on
+//    v_mfma_f32_16x16x32_bf16 (16x the f32 rate) with the six partial products whose weight is
+//    >= 2^-16: x0w0 into one fp32 accumulator, x0w1 + x1w0 + x1w1 + x0w2 + x2w0 into a second.
+//    The dropped terms (x1w2, x2w1, x2w2) are <= ~2^-24 of |x w|, i.e. below one fp32 rounding of
+//    the product, so the error matches an fp32 GEMM's (tests/test_gpu_network.py measures both
+//    against fp64). This is fp32 arithmetic emulated on the bf16 matrix cores, not a bf16 net:
+//    activations stay fp32 between layers (stored as their exact 3-part split), weights are
+//    split once per parameter update (rvz_resnet_split_weights).
 //
-// Layout (one workgroup = 4 waves = NBOARD boards; F filters; 8x8 boards):
+// Why one kernel: with MIOpen, every conv layer is a separate launch plus a zero-fill of its
+// output and a bias/skip/ReLU pass, and every activation makes an HBM round trip. Here a
+// workgroup keeps its boards' activations in LDS for the whole network: HBM traffic is the leaf
+// planes in and the logits/value out; weights stream from L2 (shared by every workgroup).
+//
+// f32 kernel layout (one workgroup = 4 waves = NBOARD boards; F filters; 8x8 boards):
 //   LDS act[2][NBOARD][64 pixels][F + 4 floats]   (ping-pong h / y; no halo: taps that leave the
 //   board are masked to 0). A pixel row is F + 4 floats, so consecutive pixels start 4 banks apart.
 //   conv layer = GEMM  M = NBOARD*64 pixels, N = F, K = 9 taps x F channels, on
@@ -17,7 +28,9 @@
 //   ds_read_b128 then reads 16 distinct consecutive pixels: bank-conflict free (a 16x16x4 layout
 //   mixed k-slots inside a group: 61% of its LDS cycles were conflicts, rocprof SQ_LDS_BANK_CONFLICT).
 //   Wave w: N-tile, 2 M-tiles -> 2 accumulators of 16 floats.
-// Packed parameter buffer (fp32, BN folded by rvz.LeafEvaluator; offsets in rvz_resnet_layout):
+// Split kernel layout: see CfgS / conv_split below.
+// Packed parameter buffer (fp32, BN folded by rvz.LeafEvaluator; every segment starts 16-byte
+// aligned; offsets in make_layout):
 //   stem_w[F][27] (k = tap*3 + ch), stem_b[F], res_w[2NB][9][F(n)][F(k)], res_b[2NB][F],
 //   pol_w[2][F], pol_b[2], pfc_w[65][128] (in = c*64 + px), pfc_b[65], val_w[F], val_b[1],
 //   vfc1_w[256][64], vfc1_b[256], vfc2_w[256], vfc2_b[1].
@@ -27,36 +40,351 @@
 
 #include "../../include/rvz.h"
 
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 struct Layout {
     int64_t stem_w, stem_b, res_w, res_b, pol_w, pol_b, pfc_w, pfc_b, val_w, val_b, vfc1_w,
         vfc1_b, vfc2_w, vfc2_b, total;
 };
 
+__host__ __device__ inline int64_t al4(int64_t o) { return (o + 3) & ~int64_t(3); }
+
 __host__ __device__ inline Layout make_layout(int F, int NB) {
     Layout L;
     int64_t o = 0;
-    L.stem_w = o; o += (int64_t)F * 27;
-    L.stem_b = o; o += F;
-    o = (o + 3) & ~int64_t(3);
-    L.res_w = o; o += (int64_t)2 * NB * 9 * F * F;
-    L.res_b = o; o += (int64_t)2 * NB * F;
-    L.pol_w = o; o += 2 * F;
-    L.pol_b = o; o += 2;
-    L.pfc_w = o; o += 65 * 128;
-    L.pfc_b = o; o += 65;
-    L.val_w = o; o += F;
-    L.val_b = o; o += 1;
-    L.vfc1_w = o; o += 256 * 64;
-    L.vfc1_b = o; o += 256;
-    L.vfc2_w = o; o += 256;
-    L.vfc2_b = o; o += 1;
+    L.stem_w = o; o = al4(o + (int64_t)F * 27);
+    L.stem_b = o; o = al4(o + F);
+    L.res_w = o;  o = al4(o + (int64_t)2 * NB * 9 * F * F);
+    L.res_b = o;  o = al4(o + (int64_t)2 * NB * F);
+    L.pol_w = o;  o = al4(o + 2 * F);
+    L.pol_b = o;  o = al4(o + 2);
+    L.pfc_w = o;  o = al4(o + 65 * 128);
+    L.pfc_b = o;  o = al4(o + 65);
+    L.val_w = o;  o = al4(o + F);
+    L.val_b = o;  o = al4(o + 1);
+    L.vfc1_w = o; o = al4(o + 256 * 64);
+    L.vfc1_b = o; o = al4(o + 256);
+    L.vfc2_w = o; o = al4(o + 256);
+    L.vfc2_b = o; o = al4(o + 1);
     L.total = o;
     return L;
 }
+
+// ---------------------------------------------------------------------------------------------
+// exact 3-part bf16 split of an fp32 value
+
+__device__ __forceinline__ uint32_t bf16_rne(float x) {      // finite x
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ float bf16_f(uint32_t h) { return __uint_as_float(h << 16); }
+
+// x == h0 + (h1 + h2) exactly: x - h0 is exact (Sterbenz), carries <= 16 significant bits, and
+// its remainder after rounding to 8 bits carries <= 8, so h2 is exact too.
+__device__ __forceinline__ void split3(float x, uint16_t& h0, uint16_t& h1, uint16_t& h2) {
+    const uint32_t b0 = bf16_rne(x);
+    const float r1 = x - bf16_f(b0);
+    const uint32_t b1 = bf16_rne(r1);
+    const float r2 = r1 - bf16_f(b1);
+    h0 = (uint16_t)b0;
+    h1 = (uint16_t)b1;
+    h2 = (uint16_t)bf16_rne(r2);
+}
+__device__ __forceinline__ float join3(uint16_t h0, uint16_t h1, uint16_t h2) {
+    return bf16_f(h0) + (bf16_f(h1) + bf16_f(h2));
+}
+
+// the same split for two values with v_cvt_pk_bf16_f32 (round to nearest even, as bf16_rne)
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 bf16x2_f(uint32_t h) {
+    return f32x2{__uint_as_float(h << 16), __uint_as_float(h & 0xFFFF0000u)};
+}
+__device__ __forceinline__ uint32_t cvt2(f32x2 x) {
+    const bf16x2 b = __builtin_convertvector(x, bf16x2);
+    return __builtin_bit_cast(uint32_t, b);
+}
+__device__ __forceinline__ void split3x2(f32x2 x, uint32_t& h0, uint32_t& h1, uint32_t& h2) {
+    h0 = cvt2(x);
+    const f32x2 r1 = x - bf16x2_f(h0);
+    h1 = cvt2(r1);
+    h2 = cvt2(r1 - bf16x2_f(h1));
+}
+
+// ---------------------------------------------------------------------------------------------
+// activation accessors: the stem writes, the heads read, through these
+
+struct ActF32 {
+    float* p;
+    int cs;
+    __device__ void store(int row, int n, float v) const { p[row * cs + n] = v; }
+    __device__ float load(int row, int k) const { return p[row * cs + k]; }
+    __device__ void load8(int row, int k0, float (&v)[8]) const {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(p + row * cs + k0);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(p + row * cs + k0 + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+    }
+};
+
+struct ActSplit {
+    uint16_t* p;
+    int cs, plane;
+    __device__ void store(int row, int n, float v) const {
+        uint16_t a, b, c;
+        split3(v, a, b, c);
+        uint16_t* o = p + row * cs + n;
+        o[0] = a;
+        o[plane] = b;
+        o[2 * plane] = c;
+    }
+    __device__ float load(int row, int k) const {
+        const uint16_t* o = p + row * cs + k;
+        return join3(o[0], o[plane], o[2 * plane]);
+    }
+    __device__ void load8(int row, int k0, float (&v)[8]) const {
+        typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+        const uint16_t* o = p + row * cs + k0;
+        const u16x8 a = *reinterpret_cast<const u16x8*>(o);
+        const u16x8 b = *reinterpret_cast<const u16x8*>(o + plane);
+        const u16x8 c = *reinterpret_cast<const u16x8*>(o + 2 * plane);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = join3(a[j], b[j], c[j]);
+    }
+};
+
+// leaf planes x[g][3][8][8] -> xin[b][10x10 padded pixel][4] (halo 0)
+template <int NBOARD>
+__device__ __forceinline__ void load_input(const float* __restrict__ x, int n_boards, int g0,
+                                           float* xin, int tid, int nthr) {
+    for (int i = tid; i < NBOARD * 100 * 4; i += nthr) xin[i] = 0.0f;
+    __syncthreads();
+    for (int i = tid; i < NBOARD * 192; i += nthr) {
+        const int b = i / 192, rem = i % 192, ch = rem / 64, px = rem % 64;
+        const int g = g0 + b;
+        const float v = g < n_boards ? x[(size_t)g * 192 + rem] : 0.0f;
+        xin[(b * 100 + (px / 8 + 1) * 10 + (px % 8) + 1) * 4 + ch] = v;
+    }
+}
+
+// stem: conv 3 -> F (VALU; 0.4% of the FLOPs), bias, ReLU -> act rows b*64 + px.
+// Lane = pixel (the 27 input taps read from LDS once), wave = (board, group of channels) with the
+// group's weights wave-uniform (scalar loads).
+template <int F, int NBOARD, int NTHR, class Act>
+__device__ __forceinline__ void stem(const float* xin, const Act& act, const float* __restrict__ prm,
+                                     const Layout& L, int tid) {
+    constexpr int NW = NTHR / 64, CG = NW / NBOARD, CPG = F / CG;
+    static_assert(NW % NBOARD == 0 && F % CG == 0, "wave -> (board, channel group)");
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), px = tid & 63;
+    const int b = wave % NBOARD, cg = wave / NBOARD, r = px >> 3, c = px & 7;
+    float in[27];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch)
+            in[t * 3 + ch] = xin[(b * 100 + (r + t / 3) * 10 + (c + t % 3)) * 4 + ch];
+    const float* w = prm + L.stem_w + (int64_t)cg * CPG * 27;
+    const float* bias = prm + L.stem_b + cg * CPG;
+#pragma unroll 4
+    for (int j = 0; j < CPG; ++j) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 27; ++k) acc = fmaf(in[k], w[j * 27 + k], acc);
+        act.store(b * 64 + px, cg * CPG + j, fmaxf(acc + bias[j], 0.0f));
+    }
+}
+
+// heads (network.py:104-117), part 1: the 1x1 convs (BN folded) + ReLU of both heads, in one
+// pass over the activations: lane = pixel, wave = (board, channel group), partial sums per group
+// through LDS (`part`, the free ping-pong buffer) added in a fixed order. Writes, per board b,
+// hpv(b)[0..127] = the policy planes (NCHW flatten, the FC's input order) and hpv(b)[128..191] =
+// the value plane.
+template <int F, int NBOARD, int NTHR, class Act, class Out>
+__device__ __forceinline__ void head_convs(const Act& act, float* part,
+                                           const float* __restrict__ prm, const Layout& L,
+                                           const Out& hpv, int tid) {
+    constexpr int NW = NTHR / 64, CG = NW / NBOARD, CPG = F / CG;
+    static_assert(CPG % 8 == 0, "8-channel reads");
+    const int lane = tid & 63;
+    {
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        const int b = wave % NBOARD, cg = wave / NBOARD, row = b * 64 + lane;
+        const float* w0 = prm + L.pol_w + cg * CPG;
+        const float* w1 = w0 + F;
+        const float* w2 = prm + L.val_w + cg * CPG;
+        float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
+#pragma unroll
+        for (int k8 = 0; k8 < CPG / 8; ++k8) {
+            float v[8];
+            act.load8(row, cg * CPG + 8 * k8, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                p0 = fmaf(v[j], w0[8 * k8 + j], p0);
+                p1 = fmaf(v[j], w1[8 * k8 + j], p1);
+                p2 = fmaf(v[j], w2[8 * k8 + j], p2);
+            }
+        }
+        part[(cg * 3 + 0) * NBOARD * 64 + row] = p0;
+        part[(cg * 3 + 1) * NBOARD * 64 + row] = p1;
+        part[(cg * 3 + 2) * NBOARD * 64 + row] = p2;
+    }
+    __syncthreads();
+    for (int o = tid; o < NBOARD * 192; o += NTHR) {
+        const int c2 = o / (NBOARD * 64), row = o % (NBOARD * 64);   // row = b*64 + px
+        float acc = 0.0f;
+#pragma unroll
+        for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * NBOARD * 64 + row];
+        const int b = row >> 6, px = row & 63;
+        const float bias = c2 < 2 ? prm[L.pol_b + c2] : prm[L.val_b];
+        hpv.store(b, c2 * 64 + px, fmaxf(acc + bias, 0.0f));
+    }
+}
+
+struct HeadsLds {        // hpv rows in LDS
+    float* p;
+    __device__ void store(int b, int i, float v) const { p[b * 192 + i] = v; }
+};
+struct HeadsGlobal {     // hpv rows in the global workspace of rvz_resnet_fwd_split
+    float* p;
+    int g0, n_boards;
+    __device__ void store(int b, int i, float v) const {
+        if (g0 + b < n_boards) p[(size_t)(g0 + b) * 192 + i] = v;
+    }
+};
+
+// heads, part 2 (in-kernel form): policy fc (128 -> 65), value fc1 (64 -> 256, ReLU), value fc2
+// (256 -> 1) + tanh, for the NBOARD boards of a workgroup; hpv in LDS
+template <int NBOARD, int NTHR>
+__device__ __forceinline__ void head_fcs(const float* hpv, float* h1,
+                                         const float* __restrict__ prm, const Layout& L, int g0,
+                                         int n_boards, float* __restrict__ logits,
+                                         float* __restrict__ value, int tid) {
+    const int lane = tid & 63;
+    // thread per output row, f32x4 loads
+    for (int o = tid; o < NBOARD * (65 + 256); o += NTHR) {
+        const int b = o / 321, rem = o % 321;
+        const int g = g0 + b;
+        if (rem < 65) {
+            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.pfc_w + rem * 128);
+            const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192);
+            float acc = prm[L.pfc_b + rem];
+#pragma unroll 16
+            for (int i = 0; i < 32; ++i) {
+                const f32x4 w = wr[i], v = in[i];
+                acc = fmaf(v[0], w[0], acc);
+                acc = fmaf(v[1], w[1], acc);
+                acc = fmaf(v[2], w[2], acc);
+                acc = fmaf(v[3], w[3], acc);
+            }
+            if (g < n_boards) logits[(size_t)g * 65 + rem] = acc;
+        } else {
+            const int u = rem - 65;
+            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + u * 64);
+            const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192 + 128);
+            float acc = prm[L.vfc1_b + u];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const f32x4 w = wr[i], v = in[i];
+                acc = fmaf(v[0], w[0], acc);
+                acc = fmaf(v[1], w[1], acc);
+                acc = fmaf(v[2], w[2], acc);
+                acc = fmaf(v[3], w[3], acc);
+            }
+            h1[b * 256 + u] = fmaxf(acc, 0.0f);
+        }
+    }
+    __syncthreads();
+    // value fc2 (256 -> 1) + tanh: one wave per board
+    const int wave = tid >> 6;
+    for (int b = wave; b < NBOARD; b += NTHR / 64) {
+        float acc = 0.0f;
+        for (int i = lane; i < 256; i += 64) acc = fmaf(h1[b * 256 + i], prm[L.vfc2_w + i], acc);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+        const int g = g0 + b;
+        if (lane == 0 && g < n_boards) value[g] = tanhf(acc + prm[L.vfc2_b]);
+    }
+}
+
+// heads, part 2 as its own launch over FCB boards per workgroup (the split path): each FC weight
+// row is loaded once per workgroup into registers and applied to all FCB boards (LDS broadcast
+// inputs) — inside the trunk kernel the same weights streamed from L2 once per 2 boards, with
+// the matrix cores idle. Thread t: value-fc1 row t; threads < 130: half of policy row t/2.
+constexpr int FCB = 16;
+__global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work, int n,
+                                                  const float* __restrict__ prm, Layout L,
+                                                  float* __restrict__ logits,
+                                                  float* __restrict__ value) {
+    __shared__ __attribute__((aligned(16))) float in[FCB][192];
+    __shared__ __attribute__((aligned(16))) float h1[FCB][256];
+    __shared__ float pp[FCB][130];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g0 = blockIdx.x * FCB, nb = n - g0 < FCB ? n - g0 : FCB;
+    f32x4 wv[16], wp[16];
+    {
+        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + tid * 64);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wv[i] = r[i];
+    }
+    if (tid < 130) {
+        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.pfc_w + (tid >> 1) * 128 +
+                                                         (tid & 1) * 64);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wp[i] = r[i];
+    }
+    for (int i = tid; i < FCB * 192; i += 256)
+        (&in[0][0])[i] = i < nb * 192 ? work[(size_t)g0 * 192 + i] : 0.0f;
+    __syncthreads();
+    const float b1 = prm[L.vfc1_b + tid];
+    for (int b = 0; b < FCB; ++b) {
+        const f32x4* v = reinterpret_cast<const f32x4*>(&in[b][128]);
+        float acc = b1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const f32x4 x = v[i];
+            acc = fmaf(x[0], wv[i][0], acc);
+            acc = fmaf(x[1], wv[i][1], acc);
+            acc = fmaf(x[2], wv[i][2], acc);
+            acc = fmaf(x[3], wv[i][3], acc);
+        }
+        h1[b][tid] = fmaxf(acc, 0.0f);
+    }
+    if (tid < 130) {
+        for (int b = 0; b < FCB; ++b) {
+            const f32x4* v = reinterpret_cast<const f32x4*>(&in[b][(tid & 1) * 64]);
+            float acc = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const f32x4 x = v[i];
+                acc = fmaf(x[0], wp[i][0], acc);
+                acc = fmaf(x[1], wp[i][1], acc);
+                acc = fmaf(x[2], wp[i][2], acc);
+                acc = fmaf(x[3], wp[i][3], acc);
+            }
+            pp[b][tid] = acc;
+        }
+    }
+    __syncthreads();
+    for (int o = tid; o < nb * 65; o += 256) {
+        const int b = o / 65, r = o % 65;
+        logits[(size_t)(g0 + b) * 65 + r] = prm[L.pfc_b + r] + (pp[b][2 * r] + pp[b][2 * r + 1]);
+    }
+    for (int b = wave; b < nb; b += 4) {
+        float acc = 0.0f;
+        for (int i = lane; i < 256; i += 64) acc = fmaf(h1[b][i], prm[L.vfc2_w + i], acc);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+        if (lane == 0) value[g0 + b] = tanhf(acc + prm[L.vfc2_b]);
+    }
+}
+
+// =============================================================================================
+// f32 MFMA kernel
 
 template <int F, int NBOARD>
 struct Cfg {
@@ -64,17 +392,14 @@ struct Cfg {
     static constexpr int BOARD = 64 * CS;            // floats per board per buffer
     static constexpr int ACT = NBOARD * BOARD;       // floats per buffer
     static constexpr int XIN = NBOARD * 100 * 4;     // stem input, 3 planes padded to 4 (halo)
-    static constexpr int HP = NBOARD * 128;          // policy conv output (NCHW flatten)
-    static constexpr int HV = NBOARD * 64;           // value conv output
+    static constexpr int HPV = NBOARD * 192;         // 1x1 conv outputs (policy NCHW, value)
     static constexpr int H1 = NBOARD * 256;          // value fc1 output
-    static constexpr int SMEM = 2 * ACT + XIN + HP + HV + H1;
+    static constexpr int SMEM = 2 * ACT + XIN + HPV + H1;
     static constexpr int MTILES = 2 * NBOARD;        // 32-pixel M-tiles (4 board rows each)
     static constexpr int NTILES = F / 32;            // 32-channel N-tiles
     static_assert(MTILES * NTILES == 8, "8 tiles = 4 waves x 2 accumulators");
     static_assert(SMEM * 4 <= 160 * 1024, "fits the 160 KiB LDS of a CU");
 };
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // One 3x3 conv layer: out = relu(conv(in) + bias (+ res)), all in LDS.
 template <int F, int NBOARD, bool RES>
@@ -139,44 +464,15 @@ __global__ __launch_bounds__(256, 2) void k_resnet_fwd(const float* __restrict__
     float* actA = smem;
     float* actB = smem + C::ACT;
     float* xin = smem + 2 * C::ACT;
-    float* hp = xin + C::XIN;
-    float* hv = hp + C::HP;
-    float* h1 = hv + C::HV;
+    float* hpv = xin + C::XIN;
+    float* h1 = hpv + C::HPV;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g0 = blockIdx.x * NBOARD;
 
-    // zero the stem input (its halo stays 0; the interior is written below)
-    for (int i = tid; i < NBOARD * 100 * 4; i += 256) xin[i] = 0.0f;
+    load_input<NBOARD>(x, n_boards, g0, xin, tid, 256);
     __syncthreads();
-    for (int i = tid; i < NBOARD * 192; i += 256) {       // x[g][ch][r][c] -> xin[b][pad px][ch]
-        const int b = i / 192, rem = i % 192, ch = rem / 64, px = rem % 64;
-        const int g = g0 + b;
-        const float v = g < n_boards ? x[(size_t)g * 192 + rem] : 0.0f;
-        xin[(b * 100 + (px / 8 + 1) * 10 + (px % 8) + 1) * 4 + ch] = v;
-    }
+    stem<F, NBOARD, 256>(xin, ActF32{actA, C::CS}, prm, L, tid);
     __syncthreads();
-
-    // stem: conv 3 -> F (VALU; 0.4% of the FLOPs), bias, ReLU -> actA
-    {
-        const int n = tid % F;
-        float wv[27];
-#pragma unroll
-        for (int k = 0; k < 27; ++k) wv[k] = prm[L.stem_w + n * 27 + k];
-        const float bn = prm[L.stem_b + n];
-        for (int pi = tid / F; pi < NBOARD * 64; pi += 256 / F) {
-            const int b = pi / 64, px = pi % 64, r = px / 8, c = px % 8;
-            float acc = 0.0f;
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const float* src = xin + (b * 100 + (r + t / 3) * 10 + (c + t % 3)) * 4;
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) acc = fmaf(src[ch], wv[t * 3 + ch], acc);
-            }
-            actA[(b * 64 + px) * C::CS + n] = fmaxf(acc + bn, 0.0f);
-        }
-    }
-    __syncthreads();
-
     for (int blk = 0; blk < n_blocks; ++blk) {
         const int l1 = 2 * blk, l2 = 2 * blk + 1;
         conv_layer<F, NBOARD, false>(actA, actB, prm + L.res_w + (size_t)l1 * 9 * F * F,
@@ -186,45 +482,304 @@ __global__ __launch_bounds__(256, 2) void k_resnet_fwd(const float* __restrict__
                                     prm + L.res_b + (size_t)l2 * F, wave, lane);
         __syncthreads();
     }
+    head_convs<F, NBOARD, 256>(ActF32{actA, C::CS}, actB, prm, L, HeadsLds{hpv}, tid);
+    __syncthreads();
+    head_fcs<NBOARD, 256>(hpv, h1, prm, L, g0, n_boards, logits, value, tid);
+}
 
-    // heads (network.py:104-117): 1x1 convs (BN folded) + ReLU
-    for (int o = tid; o < NBOARD * 192; o += 256) {
-        const int b = o / 192, rem = o % 192;
-        const int c2 = rem / 64, px = rem % 64;            // c2 0,1: policy planes; 2: value
-        const float* a = actA + (b * 64 + px) * C::CS;
-        const float* wr = c2 < 2 ? prm + L.pol_w + c2 * F : prm + L.val_w;
-        float acc = 0.0f;
-        for (int k = 0; k < F; ++k) acc = fmaf(a[k], wr[k], acc);
-        if (c2 < 2) hp[b * 128 + c2 * 64 + px] = fmaxf(acc + prm[L.pol_b + c2], 0.0f);
-        else hv[b * 64 + px] = fmaxf(acc + prm[L.val_b], 0.0f);
-    }
-    __syncthreads();
-    // policy fc (128 -> 65) and value fc1 (64 -> 256, ReLU)
-    for (int o = tid; o < NBOARD * (65 + 256); o += 256) {
-        const int b = o / 321, rem = o % 321;
-        const int g = g0 + b;
-        if (rem < 65) {
-            const float* wr = prm + L.pfc_w + rem * 128;
-            float acc = prm[L.pfc_b + rem];
-            for (int i = 0; i < 128; ++i) acc = fmaf(hp[b * 128 + i], wr[i], acc);
-            if (g < n_boards) logits[(size_t)g * 65 + rem] = acc;
-        } else {
-            const int u = rem - 65;
-            const float* wr = prm + L.vfc1_w + u * 64;
-            float acc = prm[L.vfc1_b + u];
-            for (int i = 0; i < 64; ++i) acc = fmaf(hv[b * 64 + i], wr[i], acc);
-            h1[b * 256 + u] = fmaxf(acc, 0.0f);
-        }
-    }
-    __syncthreads();
-    // value fc2 (256 -> 1) + tanh: one wave per board
-    for (int b = wave; b < NBOARD; b += 4) {
-        float acc = 0.0f;
-        for (int i = lane; i < 256; i += 64) acc = fmaf(h1[b * 256 + i], prm[L.vfc2_w + i], acc);
+// =============================================================================================
+// split (3 x bf16) kernel
+//
+// LDS: act[2 buffers][3 parts][NBOARD*64 + 1 rows][F + 8 bf16]. Row NBOARD*64 stays zero: the
+// off-board taps of the 3x3 conv read it (no halo, no select). A row is F + 8 bf16 = an odd
+// number S of 16-byte slots. A ds_read_b128 is serviced in the lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32 for the other half); here a half-wave reads 32 consecutive pixels at
+// one k-offset, so each group holds 16 pixels covering all residues mod 16 and slot(px) =
+// S*px mod 16 is distinct inside the group: conflict-free.
+// GEMM per conv layer, computed transposed (D = W X^T) on v_mfma_f32_32x32x16_bf16: M = F output
+// channels (32-channel tiles), N = NBOARD*64 pixels (32-pixel tiles), K = 9 taps x F (16-channel
+// k-steps). 8 waves, one 32x32 output tile each (F=64: 2 channel x 4 pixel tiles over 2 boards;
+// F=128: 4 x 2 over 1 board); per k-step a wave reads 3 activation fragments (LDS), loads 3
+// weight fragments (L2, prefetched two k-steps ahead) and issues 6 MFMAs (192 cycles), which
+// leaves most of each MFMA's issue gap free for the loads.
+// Lane maps: A lane l = out-channel l&31, in-channels 8(l>>5)..+7 (weights); B lane l = pixel
+// l&31, in-channels 8(l>>5)..+7 (activations); D col = l&31 = pixel, row = (reg&3) + 8(reg>>2) +
+// 4(l>>5) = out-channel: a lane ends with 4 runs of 4 consecutive channels of one pixel, stored
+// with 8-byte writes.
+// Split weights (rvz_resnet_split_weights): frag[layer][tap][kstep][part][ctile][lane][8] bf16,
+// so one wave's fragment is 1 KiB contiguous (one coalesced global_load_dwordx4 per lane).
+
+#ifdef RVZ_PHASE_TIMING   // tools/phase_timing.py: per-workgroup s_memtime at phase boundaries
+__device__ uint64_t g_phase[65536][8];
+__device__ uint64_t g_wave[65536][16];
+#define PHASE(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
+#define WAVE_T(i) \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 65536) \
+        g_wave[blockIdx.x][(threadIdx.x >> 6) + 8 * (i)] = __builtin_amdgcn_s_memtime()
+#else
+#define PHASE(i)
+#define WAVE_T(i)
+#endif
+
+template <int F, int NBOARD>
+struct CfgS {
+    static constexpr int CSB = F + 8;                // bf16 per pixel row
+    static constexpr int ZROW = NBOARD * 64;         // the zero row
+    static constexpr int PLANE = (ZROW + 1) * CSB;   // bf16 per part
+    static constexpr int ACT = 3 * PLANE;            // bf16 per buffer
+    static constexpr int XIN = NBOARD * 100 * 4;     // floats
+    static constexpr int BYTES = 2 * ACT * 2 + 4 * XIN;
+    static constexpr int KS = F / 16;                // k-steps per tap
+    static constexpr int NIT = 9 * KS;               // k-steps per layer
+    static constexpr int CT = F / 32;                // channel tiles
+    static constexpr int PT = NBOARD * 2;            // pixel tiles
+    static_assert(CT * PT == 8, "8 waves, one 32x32 tile each");
+    static_assert((CSB * 2 / 16) % 2 == 1, "odd number of 16-byte slots per row");
+    static_assert((PLANE * 2) % 16 == 0, "16-byte aligned parts");
+    static_assert(BYTES <= 160 * 1024, "fits the 160 KiB LDS of a CU");
+};
+
+#ifndef RVZ_SPLIT_TPW
+#define RVZ_SPLIT_TPW 2      // 32x32 tiles per wave
+#endif
+#ifndef RVZ_SPLIT_PD
+#define RVZ_SPLIT_PD 3       // weight prefetch distance, k-steps
+#endif
+#ifndef RVZ_SPLIT_INTERLEAVE
+#define RVZ_SPLIT_INTERLEAVE 1   // loads placed between the MFMAs of a k-step
+#endif
+#define RVZ_SPLIT_PAD 4      // k-steps of padding after the last layer's weights (>= PD)
+static_assert(RVZ_SPLIT_PD <= RVZ_SPLIT_PAD, "prefetch stays inside the padded buffer");
+
+__host__ __device__ inline int64_t split_layer_elems(int F) { return (int64_t)9 * F * F * 3; }
+__host__ __device__ inline int64_t split_kstep_elems(int F) { return (int64_t)3 * F * 16; }
+
+template <int F, int NBOARD, int TPW, bool RES>
+__device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
+                                           uint16_t* __restrict__ out,
+                                           const uint16_t* __restrict__ wl,   // layer fragments
+                                           const float* __restrict__ bias, int wave, int lane,
+                                           bf16x8 (&bc)[RVZ_SPLIT_PD][3], int ptag = -1) {
+    using C = CfgS<F, NBOARD>;
+    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_SPLIT_PD;
+    const int ct = wave % CT, pt0 = (wave / CT) * TPW;   // channel tile, first pixel tile
+    const int m = lane & 31, h = lane >> 5;
+    // this lane's pixel in each of the wave's pixel tiles, and the taps that stay on its board
+    int px[TPW];
+    unsigned pmask[TPW];
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-        const int g = g0 + b;
-        if (lane == 0 && g < n_boards) value[g] = tanhf(acc + prm[L.vfc2_b]);
+    for (int u = 0; u < TPW; ++u) {
+        px[u] = (pt0 + u) * 32 + m;
+        const int rr = (px[u] & 63) >> 3, cc = px[u] & 7;
+        unsigned msk = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            if ((unsigned)(rr + t / 3 - 1) < 8u && (unsigned)(cc + t % 3 - 1) < 8u) msk |= 1u << t;
+        pmask[u] = msk;
+    }
+    f32x16 hi[TPW], lo[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        hi[u] = f32x16{};
+        lo[u] = f32x16{};
+    }
+    // fragment (it, part) of this lane: wf[(it*3 + part)*CT*64]
+    const bf16x8* wf = reinterpret_cast<const bf16x8*>(wl) + ct * 64 + lane;
+    auto load_b = [&](bf16x8 (&bq)[3], int it) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[p] = wf[(it * 3 + p) * CT * 64];
+    };
+    auto load_a = [&](bf16x8 (&aq)[TPW][3], int it) {
+        const int t = it / KS, ks = it - t * KS;
+        const int off = (t / 3 - 1) * 8 + (t % 3 - 1);
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int row = (pmask[u] >> t) & 1u ? px[u] + off : C::ZROW;
+            const uint16_t* ap = in + row * C::CSB + ks * 16 + 8 * h;
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                aq[u][p] = *reinterpret_cast<const bf16x8*>(ap + p * C::PLANE);
+        }
+    };
+    // (weight part, activation part) of the six products, hi first; tiles interleaved so that
+    // consecutive MFMAs of one wave go to different accumulators
+    constexpr int TW[6] = {0, 0, 2, 1, 0, 1}, TA[6] = {0, 2, 0, 1, 1, 0};
+    auto compute = [&](const bf16x8 (&aq)[TPW][3], const bf16x8 (&bq)[3]) {
+#pragma unroll
+        for (int term = 0; term < 6; ++term)
+#pragma unroll
+            for (int u = 0; u < TPW; ++u) {
+                f32x16& acc = term == 0 ? hi[u] : lo[u];
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bq[TW[term]], aq[u][TA[term]], acc,
+                                                              0, 0, 0);
+            }
+    };
+    // Software pipeline, fully unrolled (constant register indices, no copies of in-flight
+    // loads): step it computes while step it+1's activation fragments (LDS) and step it+PD's
+    // weight fragments (L2) load; sched_barrier keeps the scheduler from sinking the loads next
+    // to their use. bc carries the next layer's first PD k-steps (layers are contiguous; the
+    // buffer has RVZ_SPLIT_PAD k-steps of padding after the last).
+    bf16x8 bq[NIT + PD][3];
+    bf16x8 aq[3][TPW][3];                 // activation fragments, two k-steps ahead
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[d][p] = bc[d][p];
+    load_a(aq[0], 0);
+    load_a(aq[1], 1);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        if (it + 2 < NIT) load_a(aq[(it + 2) % 3], it + 2);
+        load_b(bq[it + PD], it + PD);
+#if RVZ_SPLIT_INTERLEAVE
+        compute(aq[it % 3], bq[it]);
+        if constexpr (TPW == 2) {
+            // one load per MFMA issue gap (an MFMA leaves 24 of its 32 cycles free), instead of
+            // 9 loads back to back while the matrix pipe drains
+#define RVZ_SGB(mask) __builtin_amdgcn_sched_group_barrier(mask, 1, 0)
+            RVZ_SGB(0x008); RVZ_SGB(0x100); RVZ_SGB(0x008); RVZ_SGB(0x100);
+            RVZ_SGB(0x008); RVZ_SGB(0x100); RVZ_SGB(0x008); RVZ_SGB(0x100);
+            RVZ_SGB(0x008); RVZ_SGB(0x100); RVZ_SGB(0x008); RVZ_SGB(0x100);
+            RVZ_SGB(0x008); RVZ_SGB(0x020); RVZ_SGB(0x008); RVZ_SGB(0x020);
+            RVZ_SGB(0x008); RVZ_SGB(0x020); RVZ_SGB(0x008); RVZ_SGB(0x008);
+            RVZ_SGB(0x008); RVZ_SGB(0x008);
+#undef RVZ_SGB
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#else
+        __builtin_amdgcn_sched_barrier(0);
+        compute(aq[it % 3], bq[it]);
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bc[d][p] = bq[NIT + d][p];
+    if (ptag >= 0) {
+        PHASE(ptag);
+        WAVE_T(0);
+    }
+    // epilogue: bias (+ skip), ReLU, exact split back into the three parts; per register group
+    // g the lane holds channels ct*32 + 8g + 4h .. +3 of its pixel -> 8-byte reads/writes
+    typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n0 = ct * 32 + 8 * g + 4 * h;
+            const f32x4 bn = *reinterpret_cast<const f32x4*>(bias + n0);
+            uint16_t* o = out + px[u] * C::CSB + n0;
+            u16x4 s0, s1, s2;
+            if (RES) {
+                s0 = *reinterpret_cast<const u16x4*>(o);
+                s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
+                s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
+            }
+            u32x2 d0, d1, d2;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                f32x2 v;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int j = 2 * hf + e, reg = 4 * g + j;
+                    v[e] = (hi[u][reg] + lo[u][reg]) + bn[j];
+                    if (RES) v[e] += join3(s0[j], s1[j], s2[j]);   // skip input, in place
+                    v[e] = fmaxf(v[e], 0.0f);
+                }
+                uint32_t h0, h1, h2;
+                split3x2(v, h0, h1, h2);
+                d0[hf] = h0;
+                d1[hf] = h1;
+                d2[hf] = h2;
+            }
+            *reinterpret_cast<u32x2*>(o) = d0;
+            *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
+            *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
+        }
+}
+
+
+// TPW = 32x32 output tiles per wave: 1 -> 8 waves (two per SIMD), 2 -> 4 waves (one per SIMD,
+// each weight fragment reused over two pixel tiles)
+template <int F, int NBOARD, int TPW>
+__global__ __launch_bounds__(512 / TPW, 1) void k_resnet_split(const float* __restrict__ x,
+                                                               int n_boards,
+                                                               const float* __restrict__ prm,
+                                                               Layout L,
+                                                               const uint16_t* __restrict__ wsp,
+                                                               int n_blocks,
+                                                               float* __restrict__ work) {
+    using C = CfgS<F, NBOARD>;
+    constexpr int NTHR = 512 / TPW;
+    __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
+    uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* actB = actA + C::ACT;
+    float* xin = reinterpret_cast<float*>(actB + C::ACT);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g0 = blockIdx.x * NBOARD;
+    PHASE(0);
+
+    // zero rows of both buffers, all parts (6 consecutive planes)
+    for (int i = tid; i < 6 * C::CSB; i += NTHR) {
+        const int part = i / C::CSB, k = i % C::CSB;
+        actA[part * C::PLANE + C::ZROW * C::CSB + k] = 0;
+    }
+    // the first PD k-steps' weight fragments, in flight during the input and stem
+    bf16x8 bc[RVZ_SPLIT_PD][3];
+    if (n_blocks > 0) {
+        const bf16x8* wf = reinterpret_cast<const bf16x8*>(wsp) + (wave % C::CT) * 64 + lane;
+#pragma unroll
+        for (int s = 0; s < RVZ_SPLIT_PD; ++s)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bc[s][p] = wf[(s * 3 + p) * C::CT * 64];
+    }
+    load_input<NBOARD>(x, n_boards, g0, xin, tid, NTHR);
+    __syncthreads();
+    const ActSplit outA{actA, C::CSB, C::PLANE};
+    stem<F, NBOARD, NTHR>(xin, outA, prm, L, tid);
+    __syncthreads();
+    PHASE(1);
+    const int64_t LW = split_layer_elems(F);
+    for (int blk = 0; blk < n_blocks; ++blk) {
+        const int l1 = 2 * blk, l2 = 2 * blk + 1;
+        conv_split<F, NBOARD, TPW, false>(actA, actB, wsp + l1 * LW,
+                                          prm + L.res_b + (size_t)l1 * F, wave, lane, bc,
+                                          blk == 0 ? 4 : -1);
+        if (blk == 0) {
+            PHASE(5);
+            WAVE_T(1);
+        }
+        __syncthreads();
+        if (blk == 0) PHASE(6);
+        conv_split<F, NBOARD, TPW, true>(actB, actA, wsp + l2 * LW,
+                                         prm + L.res_b + (size_t)l2 * F, wave, lane, bc);
+        __syncthreads();
+    }
+    PHASE(2);
+    head_convs<F, NBOARD, NTHR>(outA, reinterpret_cast<float*>(actB), prm, L,
+                                HeadsGlobal{work, g0, n_boards}, tid);
+    PHASE(3);
+}
+
+// res_w[l][t][n][k] fp32 -> frag[l][t][ks][part][ctile][lane][8] bf16 parts
+__global__ void k_split_weights(const float* __restrict__ w, int F, int64_t total,
+                                uint16_t* __restrict__ out) {
+    const int KS = F / 16, CT = F / 32;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(i % F), n = (int)((i / F) % F);
+        const int64_t lt = i / ((int64_t)F * F);             // layer*9 + tap
+        const int ks = k / 16, hh = (k % 16) / 8, j = k % 8, ct = n / 32, mm = n % 32;
+        const int ln = hh * 32 + mm;
+        uint16_t h[3];
+        split3(w[i], h[0], h[1], h[2]);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            out[((((lt * KS + ks) * 3 + p) * CT + ct) * 64 + ln) * 8 + j] = h[p];
     }
 }
 
@@ -255,6 +810,65 @@ int rvz_resnet_fwd_f32(const float* x, int32_t n, const float* params, int32_t f
     } else {
         return RVZ_EINVAL;
     }
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+#ifdef RVZ_PHASE_TIMING
+int rvz_wave_read(uint64_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave), (size_t)n * 16 * sizeof(uint64_t)) ==
+                   hipSuccess ? 0 : -5;
+}
+int rvz_phase_read(uint64_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_phase), (size_t)n * 8 * sizeof(uint64_t)) ==
+                   hipSuccess ? 0 : -5;
+}
+#endif
+
+int64_t rvz_resnet_split_size(int32_t filters, int32_t blocks) {
+    if ((filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
+    // + padding: the last layer's weight prefetch runs up to RVZ_SPLIT_PAD steps past the end
+    return (int64_t)2 * blocks * split_layer_elems(filters) +
+           RVZ_SPLIT_PAD * split_kstep_elems(filters);
+}
+
+int rvz_resnet_split_weights(const float* params, int32_t filters, int32_t blocks, uint16_t* out,
+                             void* stream) {
+    if (!params || (!out && blocks > 0) || (filters != 64 && filters != 128) || blocks < 0)
+        return RVZ_EINVAL;
+    if (blocks == 0) return RVZ_OK;
+    const Layout L = make_layout(filters, blocks);
+    const int64_t total = (int64_t)2 * blocks * 9 * filters * filters;
+    const int64_t nblk = (total + 255) / 256;
+    hipLaunchKernelGGL(k_split_weights, dim3((unsigned)(nblk < 4096 ? nblk : 4096)), dim3(256), 0,
+                       (hipStream_t)stream, params + L.res_w, filters, total, out);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192; }
+
+int rvz_resnet_fwd_split(const float* x, int32_t n, const float* params, const uint16_t* wsplit,
+                         int32_t filters, int32_t blocks, float* work, float* logits,
+                         float* value, void* stream) {
+    if (!x || !params || (!wsplit && blocks > 0) || !work || !logits || !value || n < 0 ||
+        blocks < 0)
+        return RVZ_EINVAL;
+    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)wsplit & 15) != 0) return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    const Layout L = make_layout(filters, blocks);
+    hipStream_t s = (hipStream_t)stream;
+    if (filters == 64) {
+        hipLaunchKernelGGL((k_resnet_split<64, 2, RVZ_SPLIT_TPW>), dim3((n + 1) / 2),
+                           dim3(512 / RVZ_SPLIT_TPW), 0, s, x, n, params, L, wsplit, blocks,
+                           work);
+    } else if (filters == 128) {
+        hipLaunchKernelGGL((k_resnet_split<128, 1, RVZ_SPLIT_TPW>), dim3(n),
+                           dim3(512 / RVZ_SPLIT_TPW), 0, s, x, n, params, L, wsplit, blocks,
+                           work);
+    } else {
+        return RVZ_EINVAL;
+    }
+    hipLaunchKernelGGL(k_heads_fc, dim3((n + FCB - 1) / FCB), dim3(256), 0, s, work, n, params, L,
+                       logits, value);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 

@@ -66,6 +66,11 @@ SIGNATURES = {
     "rvz_nn_bias_act_bf16": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
     "rvz_resnet_params_size": (C.c_int64, [C.c_int32, C.c_int32]),
     "rvz_resnet_fwd_f32": (C.c_int, [_P, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P, _P]),
+    "rvz_resnet_split_size": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rvz_resnet_split_weights": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
+    "rvz_resnet_work_size": (C.c_int64, [C.c_int32]),
+    "rvz_resnet_fwd_split": (C.c_int, [_P, C.c_int32, _P, _P, C.c_int32, C.c_int32, _P, _P, _P,
+                                       _P]),
 }
 
 _lib = None

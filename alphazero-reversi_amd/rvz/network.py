@@ -106,25 +106,23 @@ def pack_resnet_params(net: AlphaZeroNetwork) -> torch.Tensor:
     F = net.num_filters
     parts = []
 
-    def put(t):
-        parts.append(t.detach().float().reshape(-1))
+    def put(t):                                            # every segment 16-byte aligned
+        t = t.detach().float().reshape(-1)
+        parts.append(t)
+        if t.numel() % 4:
+            parts.append(torch.zeros(4 - t.numel() % 4, device=t.device))
 
     w, b = _fold(net.conv, net.bn)                         # [F,3,3,3] -> [F][tap*3 + ch]
     put(w.permute(0, 2, 3, 1).reshape(F, 27))
     put(b)
-    n = sum(x.numel() for x in parts)
-    if n % 4:
-        parts.append(torch.zeros(4 - n % 4, device=w.device))
     ws, bs = [], []
     for blk in net.res_blocks:
         for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
             w, b = _fold(conv, bn)                         # [n][k][3][3] -> [tap][n][k]
             ws.append(w.permute(2, 3, 0, 1).reshape(9, F, F))
             bs.append(b)
-    for t in ws:
-        put(t)
-    for t in bs:
-        put(t)
+    put(torch.stack(ws) if ws else torch.zeros(0, device=w.device))
+    put(torch.stack(bs) if bs else torch.zeros(0, device=w.device))
     w, b = _fold(net.policy_conv, net.policy_bn)
     put(w.reshape(2, F))
     put(b)
@@ -153,22 +151,37 @@ class LeafEvaluator:
         net = net.eval()
         dev = torch.device(device) if device is not None else next(net.parameters()).device
         self.dtype, self.device = dtype, dev
-        # kernel: "resnet" = the whole forward in rvz_resnet_fwd_f32 (fp32, 8x8, 64/128 filters),
-        # "miopen" = PyTorch convs (+ the fused epilogue), "auto" = resnet where it applies
+        # kernel: the whole forward in one rvz kernel (fp32, 8x8, 64/128 filters) —
+        #   "split" = fp32 emulated exactly-split on the bf16 MFMA (rvz_resnet_fwd_split),
+        #   "resnet" = the f32-input MFMA (rvz_resnet_fwd_f32);
+        # "miopen" = PyTorch convs (+ the fused epilogue); "auto" = split where it applies
         self.n_blocks, self.filters = len(net.res_blocks), net.num_filters
         resnet_ok = (dev.type == "cuda" and dtype == torch.float32 and net.board_size == 8
                      and net.num_filters in (64, 128))
-        if kernel == "resnet" and not resnet_ok:
-            raise ValueError("the fused resnet kernel needs fp32, 8x8, 64 or 128 filters, a GPU")
-        self.use_resnet = kernel == "resnet" or (kernel == "auto" and resnet_ok)
+        if kernel not in ("auto", "split", "resnet", "miopen"):
+            raise ValueError(f"unknown kernel {kernel!r}")
+        if kernel in ("split", "resnet") and not resnet_ok:
+            raise ValueError("the fused resnet kernels need fp32, 8x8, 64 or 128 filters, a GPU")
+        if kernel == "auto":
+            kernel = "split" if resnet_ok else "miopen"
+        self.kernel = kernel
+        self.use_resnet = kernel in ("split", "resnet")
         self._outs = {}
         if self.use_resnet:
             from . import _lib
+            lib = _lib.load()
             with torch.no_grad():
                 self.params = pack_resnet_params(net).to(dev).contiguous()
-            want = _lib.load().rvz_resnet_params_size(self.filters, self.n_blocks)
+            want = lib.rvz_resnet_params_size(self.filters, self.n_blocks)
             if want != self.params.numel():
                 raise _lib.RvzError(f"packed params {self.params.numel()} != layout {want}")
+            self.wsplit = None
+            if kernel == "split":
+                n = lib.rvz_resnet_split_size(self.filters, self.n_blocks)
+                self.wsplit = torch.empty(max(n, 8), dtype=torch.int16, device=dev)
+                _lib.check(lib.rvz_resnet_split_weights(
+                    self.params.data_ptr(), self.filters, self.n_blocks, self.wsplit.data_ptr(),
+                    _lib.stream_handle(dev)), None, "rvz_resnet_split_weights")
         # on the GPU the conv bias, ReLU and skip add run in one rvz kernel pass (rvz_nn_bias_act)
         self.fused = dev.type == "cuda" if fused_epilogue is None else bool(fused_epilogue)
         self.board_size = net.board_size
@@ -224,13 +237,20 @@ class LeafEvaluator:
         outs = self._outs.get(n)
         if outs is None:   # fixed per batch size: stable addresses under HIP-graph capture
             outs = (torch.empty(n, self.board_size ** 2 + 1, device=self.device),
-                    torch.empty(n, device=self.device))
+                    torch.empty(n, device=self.device),
+                    torch.empty(max(1, _lib.load().rvz_resnet_work_size(n)), device=self.device))
             self._outs[n] = outs
-        logits, value = outs
-        _lib.check(_lib.load().rvz_resnet_fwd_f32(
-            x.data_ptr(), n, self.params.data_ptr(), self.filters, self.n_blocks,
-            logits.data_ptr(), value.data_ptr(), _lib.stream_handle(x.device)),
-            None, "rvz_resnet_fwd_f32")
+        logits, value, work = outs
+        if self.wsplit is not None:
+            _lib.check(_lib.load().rvz_resnet_fwd_split(
+                x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(), self.filters,
+                self.n_blocks, work.data_ptr(), logits.data_ptr(), value.data_ptr(),
+                _lib.stream_handle(x.device)), None, "rvz_resnet_fwd_split")
+        else:
+            _lib.check(_lib.load().rvz_resnet_fwd_f32(
+                x.data_ptr(), n, self.params.data_ptr(), self.filters, self.n_blocks,
+                logits.data_ptr(), value.data_ptr(), _lib.stream_handle(x.device)),
+                None, "rvz_resnet_fwd_f32")
         return logits, value
 
     @torch.no_grad()

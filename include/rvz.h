@@ -149,6 +149,20 @@ int64_t rvz_resnet_params_size(int32_t filters, int32_t blocks);
 int rvz_resnet_fwd_f32(const float *x, int32_t n, const float *params, int32_t filters,
                        int32_t blocks, float *logits, float *value, void *hip_stream);
 
+/* The same forward with fp32 arithmetic emulated on the bf16 MFMA: every operand split exactly
+ * into three bf16 parts (x = x0 + (x1 + x2)) and the six partial products of weight >= 2^-16
+ * accumulated in fp32 (error of an fp32 GEMM; see csrc/rvz_resnet.hip). wsplit: the conv weights
+ * re-laid out by rvz_resnet_split_weights from the packed params (once per parameter update),
+ * rvz_resnet_split_size(filters, blocks) uint16 elements, 16-byte aligned. work: float scratch of
+ * rvz_resnet_work_size(n) elements (the 1x1-conv head outputs handed to the FC launch). */
+int64_t rvz_resnet_split_size(int32_t filters, int32_t blocks);
+int rvz_resnet_split_weights(const float *params, int32_t filters, int32_t blocks,
+                             uint16_t *wsplit, void *hip_stream);
+int64_t rvz_resnet_work_size(int32_t n);
+int rvz_resnet_fwd_split(const float *x, int32_t n, const float *params, const uint16_t *wsplit,
+                         int32_t filters, int32_t blocks, float *work, float *logits,
+                         float *value, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,12 +72,9 @@ def test_evaluator_fp32_matches_module(blocks, filters):
     assert (vb - vr).abs().mean().item() < 0.1      # tanh saturates: a few signs flip
 
 
-@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 4096), (10, 128, 515), (1, 64, 3), (0, 128, 2)])
-def test_resnet_kernel_matches_module(blocks, filters, n):
-    """rvz_resnet_fwd_f32 (whole forward, fp32 MFMA) vs the nn.Module (fp32): same arithmetic
-    type, different summation order; odd batch sizes cover the partial last workgroup."""
+def _bn_net(blocks, filters, seed=3):
     import rvz
-    torch.manual_seed(3)
+    torch.manual_seed(seed)
     net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
     with torch.no_grad():
         for m in net.modules():
@@ -86,13 +83,46 @@ def test_resnet_kernel_matches_module(blocks, filters, n):
                 m.running_var.uniform_(0.5, 1.5)
                 m.weight.uniform_(0.5, 1.5)
                 m.bias.uniform_(-0.1, 0.1)
+    return net
+
+
+@pytest.mark.parametrize("kernel", ["resnet", "split"])
+@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 4096), (10, 128, 515), (1, 64, 3), (0, 128, 2)])
+def test_resnet_kernel_matches_module(kernel, blocks, filters, n):
+    """rvz_resnet_fwd_f32 (f32 MFMA) and rvz_resnet_fwd_split (fp32 split over bf16 MFMA), whole
+    forward, vs the nn.Module (fp32): fp32-class arithmetic, different summation order; odd batch
+    sizes cover the partial last workgroup."""
+    import rvz
+    net = _bn_net(blocks, filters)
     x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
     with torch.no_grad():
         lr, vr = net(x)
-    ev = rvz.LeafEvaluator(net, kernel="resnet")
-    assert ev.use_resnet
+    ev = rvz.LeafEvaluator(net, kernel=kernel)
+    assert ev.use_resnet and ev.kernel == kernel
     l, v = ev(x)
     torch.cuda.synchronize()
     scale = lr.abs().max().item()
     assert (l - lr).abs().max().item() <= 2e-5 * scale
     assert (v - vr).abs().max().item() <= 2e-3
+
+
+@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 512), (10, 128, 128)])
+def test_split_error_is_fp32_class(blocks, filters, n):
+    """Error against an fp64 evaluation of the same module: the split kernel's must be of the
+    order of the fp32 paths' (f32 MFMA kernel, PyTorch fp32) — not bf16's (~1e-3 relative)."""
+    import rvz
+    net = _bn_net(blocks, filters, seed=5)
+    x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
+    with torch.no_grad():
+        l64, v64 = net.double().cpu()(x.double().cpu())
+        net.float().cuda()
+        lm, vm = net(x)
+    err = {}
+    for kern in ("resnet", "split"):
+        l, v = rvz.LeafEvaluator(net, kernel=kern)(x)
+        err[kern] = (l.double().cpu() - l64).abs().max().item()
+    err["module"] = (lm.double().cpu() - l64).abs().max().item()
+    scale = l64.abs().max().item()
+    fp32 = max(err["resnet"], err["module"])
+    assert err["split"] <= 4 * fp32 + 1e-7 * scale, (err, scale)
+    assert err["split"] <= 1e-5 * scale, (err, scale)
