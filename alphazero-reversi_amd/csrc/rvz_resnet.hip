@@ -315,7 +315,10 @@ __device__ __forceinline__ void head_fcs(const float* hpv, float* h1,
 // row is loaded once per workgroup into registers and applied to all FCB boards (LDS broadcast
 // inputs) — inside the trunk kernel the same weights streamed from L2 once per 2 boards, with
 // the matrix cores idle. Thread t: value-fc1 row t; threads < 130: half of policy row t/2.
-constexpr int FCB = 16;
+#ifndef RVZ_FCB
+#define RVZ_FCB 8
+#endif
+constexpr int FCB = RVZ_FCB;   // boards per workgroup (multiple of 4)
 __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work, int n,
                                                   const float* __restrict__ prm, Layout L,
                                                   float* __restrict__ logits,
@@ -340,33 +343,41 @@ __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work
     for (int i = tid; i < FCB * 192; i += 256)
         (&in[0][0])[i] = i < nb * 192 ? work[(size_t)g0 * 192 + i] : 0.0f;
     __syncthreads();
+    // 4 boards at a time: four independent FMA chains per thread
+    constexpr int IL = 4;
     const float b1 = prm[L.vfc1_b + tid];
-    for (int b = 0; b < FCB; ++b) {
-        const f32x4* v = reinterpret_cast<const f32x4*>(&in[b][128]);
-        float acc = b1;
+    for (int b0 = 0; b0 < FCB; b0 += IL) {
+        float acc[IL];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const f32x4 x = v[i];
-            acc = fmaf(x[0], wv[i][0], acc);
-            acc = fmaf(x[1], wv[i][1], acc);
-            acc = fmaf(x[2], wv[i][2], acc);
-            acc = fmaf(x[3], wv[i][3], acc);
-        }
-        h1[b][tid] = fmaxf(acc, 0.0f);
+        for (int j = 0; j < IL; ++j) acc[j] = b1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int j = 0; j < IL; ++j) {
+                const f32x4 x = reinterpret_cast<const f32x4*>(&in[b0 + j][128])[i];
+                acc[j] = fmaf(x[0], wv[i][0], acc[j]);
+                acc[j] = fmaf(x[1], wv[i][1], acc[j]);
+                acc[j] = fmaf(x[2], wv[i][2], acc[j]);
+                acc[j] = fmaf(x[3], wv[i][3], acc[j]);
+            }
+#pragma unroll
+        for (int j = 0; j < IL; ++j) h1[b0 + j][tid] = fmaxf(acc[j], 0.0f);
     }
     if (tid < 130) {
-        for (int b = 0; b < FCB; ++b) {
-            const f32x4* v = reinterpret_cast<const f32x4*>(&in[b][(tid & 1) * 64]);
-            float acc = 0.0f;
+        for (int b0 = 0; b0 < FCB; b0 += IL) {
+            float acc[IL] = {};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const f32x4 x = v[i];
-                acc = fmaf(x[0], wp[i][0], acc);
-                acc = fmaf(x[1], wp[i][1], acc);
-                acc = fmaf(x[2], wp[i][2], acc);
-                acc = fmaf(x[3], wp[i][3], acc);
-            }
-            pp[b][tid] = acc;
+            for (int i = 0; i < 16; ++i)
+#pragma unroll
+                for (int j = 0; j < IL; ++j) {
+                    const f32x4 x = reinterpret_cast<const f32x4*>(&in[b0 + j][(tid & 1) * 64])[i];
+                    acc[j] = fmaf(x[0], wp[i][0], acc[j]);
+                    acc[j] = fmaf(x[1], wp[i][1], acc[j]);
+                    acc[j] = fmaf(x[2], wp[i][2], acc[j]);
+                    acc[j] = fmaf(x[3], wp[i][3], acc[j]);
+                }
+#pragma unroll
+            for (int j = 0; j < IL; ++j) pp[b0 + j][tid] = acc[j];
         }
     }
     __syncthreads();
@@ -546,6 +557,9 @@ struct CfgS {
 #ifndef RVZ_SPLIT_PD
 #define RVZ_SPLIT_PD 3       // weight prefetch distance, k-steps
 #endif
+#ifndef RVZ_STEM_MFMA
+#define RVZ_STEM_MFMA 1          // stem conv on the split MFMA (else VALU)
+#endif
 #ifndef RVZ_SPLIT_INTERLEAVE
 #define RVZ_SPLIT_INTERLEAVE 1   // loads placed between the MFMAs of a k-step
 #endif
@@ -554,6 +568,123 @@ static_assert(RVZ_SPLIT_PD <= RVZ_SPLIT_PAD, "prefetch stays inside the padded b
 
 __host__ __device__ inline int64_t split_layer_elems(int F) { return (int64_t)9 * F * F * 3; }
 __host__ __device__ inline int64_t split_kstep_elems(int F) { return (int64_t)3 * F * 16; }
+
+// conv epilogue: bias (+ skip), ReLU, exact split back into the three parts; per register group
+// g the lane holds channels ct*32 + 8g + 4h .. +3 of its pixel -> 8-byte reads/writes
+template <int F, int NBOARD, int TPW, bool RES>
+__device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out, const f32x16 (&hi)[TPW],
+                                               const f32x16 (&lo)[TPW],
+                                               const float* __restrict__ bias, int ct,
+                                               const int (&px)[TPW], int h) {
+    using C = CfgS<F, NBOARD>;
+    typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int u = 0; u < TPW; ++u)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n0 = ct * 32 + 8 * g + 4 * h;
+            const f32x4 bn = *reinterpret_cast<const f32x4*>(bias + n0);
+            uint16_t* o = out + px[u] * C::CSB + n0;
+            u16x4 s0, s1, s2;
+            if (RES) {
+                s0 = *reinterpret_cast<const u16x4*>(o);
+                s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
+                s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
+            }
+            u32x2 d0, d1, d2;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                f32x2 v;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int j = 2 * hf + e, reg = 4 * g + j;
+                    v[e] = (hi[u][reg] + lo[u][reg]) + bn[j];
+                    if (RES) v[e] += join3(s0[j], s1[j], s2[j]);   // skip input, in place
+                    v[e] = fmaxf(v[e], 0.0f);
+                }
+                uint32_t h0, h1, h2;
+                split3x2(v, h0, h1, h2);
+                d0[hf] = h0;
+                d1[hf] = h1;
+                d2[hf] = h2;
+            }
+            *reinterpret_cast<u32x2*>(o) = d0;
+            *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
+            *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
+        }
+}
+
+// 8 bf16 parts p of 8 fp32 values
+__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&out)[3]) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 w0, w1, w2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t a, b, c;
+        split3x2(f32x2{v[2 * i], v[2 * i + 1]}, a, b, c);
+        w0[i] = a;
+        w1[i] = b;
+        w2[i] = c;
+    }
+    out[0] = __builtin_bit_cast(bf16x8, w0);
+    out[1] = __builtin_bit_cast(bf16x8, w1);
+    out[2] = __builtin_bit_cast(bf16x8, w2);
+}
+
+// stem conv 3 -> F (network.py:33-34 + BN folded) as a K = 27 (padded to 32) GEMM on the same
+// split MFMA and tile map as the trunk: k = tap*3 + ch; A = stem weights (split in registers),
+// B = the input taps read from the halo-padded xin; epilogue into actA.
+template <int F, int NBOARD, int TPW>
+__device__ __forceinline__ void stem_split(const float* xin, uint16_t* __restrict__ out,
+                                           const float* __restrict__ prm, const Layout& L,
+                                           int wave, int lane) {
+    using C = CfgS<F, NBOARD>;
+    constexpr int CT = C::CT;
+    const int ct = wave % CT, pt0 = (wave / CT) * TPW;
+    const int m = lane & 31, h = lane >> 5;
+    int px[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) px[u] = (pt0 + u) * 32 + m;
+    f32x16 hi[TPW], lo[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        hi[u] = f32x16{};
+        lo[u] = f32x16{};
+    }
+    const float* wrow = prm + L.stem_w + (ct * 32 + m) * 27;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        float wv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = ks * 16 + 8 * h + j;
+            wv[j] = k < 27 ? wrow[k] : 0.0f;
+        }
+        bf16x8 wq[3];
+        split8(wv, wq);
+#pragma unroll
+        for (int u = 0; u < TPW; ++u) {
+            const int b = px[u] >> 6, r = (px[u] & 63) >> 3, c = px[u] & 7;
+            float xv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = ks * 16 + 8 * h + j, t = k / 3, ch = k % 3;
+                xv[j] = k < 27 ? xin[(b * 100 + (r + t / 3) * 10 + (c + t % 3)) * 4 + ch] : 0.0f;
+            }
+            bf16x8 aq[3];
+            split8(xv, aq);
+            constexpr int TW[6] = {0, 0, 2, 1, 0, 1}, TA[6] = {0, 2, 0, 1, 1, 0};
+#pragma unroll
+            for (int term = 0; term < 6; ++term) {
+                f32x16& acc = term == 0 ? hi[u] : lo[u];
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[TW[term]], aq[TA[term]], acc, 0,
+                                                              0, 0);
+            }
+        }
+    }
+    epilogue_split<F, NBOARD, TPW, false>(out, hi, lo, prm + L.stem_b, ct, px, h);
+}
 
 template <int F, int NBOARD, int TPW, bool RES>
 __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
@@ -661,46 +792,8 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
         PHASE(ptag);
         WAVE_T(0);
     }
-    // epilogue: bias (+ skip), ReLU, exact split back into the three parts; per register group
-    // g the lane holds channels ct*32 + 8g + 4h .. +3 of its pixel -> 8-byte reads/writes
-    typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int u = 0; u < TPW; ++u)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n0 = ct * 32 + 8 * g + 4 * h;
-            const f32x4 bn = *reinterpret_cast<const f32x4*>(bias + n0);
-            uint16_t* o = out + px[u] * C::CSB + n0;
-            u16x4 s0, s1, s2;
-            if (RES) {
-                s0 = *reinterpret_cast<const u16x4*>(o);
-                s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
-                s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
-            }
-            u32x2 d0, d1, d2;
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                f32x2 v;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int j = 2 * hf + e, reg = 4 * g + j;
-                    v[e] = (hi[u][reg] + lo[u][reg]) + bn[j];
-                    if (RES) v[e] += join3(s0[j], s1[j], s2[j]);   // skip input, in place
-                    v[e] = fmaxf(v[e], 0.0f);
-                }
-                uint32_t h0, h1, h2;
-                split3x2(v, h0, h1, h2);
-                d0[hf] = h0;
-                d1[hf] = h1;
-                d2[hf] = h2;
-            }
-            *reinterpret_cast<u32x2*>(o) = d0;
-            *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
-            *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
-        }
+    epilogue_split<F, NBOARD, TPW, RES>(out, hi, lo, bias, ct, px, h);
 }
-
 
 // TPW = 32x32 output tiles per wave: 1 -> 8 waves (two per SIMD), 2 -> 4 waves (one per SIMD,
 // each weight fragment reused over two pixel tiles)
@@ -740,7 +833,11 @@ __global__ __launch_bounds__(512 / TPW, 1) void k_resnet_split(const float* __re
     load_input<NBOARD>(x, n_boards, g0, xin, tid, NTHR);
     __syncthreads();
     const ActSplit outA{actA, C::CSB, C::PLANE};
+#if RVZ_STEM_MFMA
+    stem_split<F, NBOARD, TPW>(xin, actA, prm, L, wave, lane);
+#else
     stem<F, NBOARD, NTHR>(xin, outA, prm, L, tid);
+#endif
     __syncthreads();
     PHASE(1);
     const int64_t LW = split_layer_elems(F);
@@ -846,11 +943,10 @@ int rvz_resnet_split_weights(const float* params, int32_t filters, int32_t block
 
 int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192; }
 
-int rvz_resnet_fwd_split(const float* x, int32_t n, const float* params, const uint16_t* wsplit,
-                         int32_t filters, int32_t blocks, float* work, float* logits,
-                         float* value, void* stream) {
-    if (!x || !params || (!wsplit && blocks > 0) || !work || !logits || !value || n < 0 ||
-        blocks < 0)
+int rvz_resnet_trunk_split(const float* x, int32_t n, const float* params,
+                           const uint16_t* wsplit, int32_t filters, int32_t blocks, float* work,
+                           void* stream) {
+    if (!x || !params || (!wsplit && blocks > 0) || !work || n < 0 || blocks < 0)
         return RVZ_EINVAL;
     if (((uintptr_t)params & 15) != 0 || ((uintptr_t)wsplit & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
@@ -867,9 +963,29 @@ int rvz_resnet_fwd_split(const float* x, int32_t n, const float* params, const u
     } else {
         return RVZ_EINVAL;
     }
-    hipLaunchKernelGGL(k_heads_fc, dim3((n + FCB - 1) / FCB), dim3(256), 0, s, work, n, params, L,
-                       logits, value);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_resnet_heads_fc(const float* work, int32_t n, const float* params, int32_t filters,
+                        int32_t blocks, float* logits, float* value, void* stream) {
+    if (!work || !params || !logits || !value || n < 0 || blocks < 0 ||
+        (filters != 64 && filters != 128))
+        return RVZ_EINVAL;
+    if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    const Layout L = make_layout(filters, blocks);
+    hipLaunchKernelGGL(k_heads_fc, dim3((n + FCB - 1) / FCB), dim3(256), 0, (hipStream_t)stream,
+                       work, n, params, L, logits, value);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_resnet_fwd_split(const float* x, int32_t n, const float* params, const uint16_t* wsplit,
+                         int32_t filters, int32_t blocks, float* work, float* logits,
+                         float* value, void* stream) {
+    if (!logits || !value) return RVZ_EINVAL;
+    const int rc = rvz_resnet_trunk_split(x, n, params, wsplit, filters, blocks, work, stream);
+    if (rc != RVZ_OK) return rc;
+    return rvz_resnet_heads_fc(work, n, params, filters, blocks, logits, value, stream);
 }
 
 }  // extern "C"

@@ -253,6 +253,26 @@ class LeafEvaluator:
                 None, "rvz_resnet_fwd_f32")
         return logits, value
 
+    def trunk_only(self, x: torch.Tensor):
+        """The split path's first launch alone (rvz_resnet_trunk_split: stem, residual tower,
+        1x1 head convs -> the workspace); bench.py times the dominant kernel with it."""
+        from . import _lib
+        if self.wsplit is None:
+            raise _lib.RvzError("trunk_only needs kernel='split'")
+        if x.shape[0] not in self._outs:
+            self(x)                                # allocates the per-batch buffers
+        work = self._outs[x.shape[0]][2]
+        _lib.check(_lib.load().rvz_resnet_trunk_split(
+            x.data_ptr(), x.shape[0], self.params.data_ptr(), self.wsplit.data_ptr(),
+            self.filters, self.n_blocks, work.data_ptr(), _lib.stream_handle(x.device)),
+            None, "rvz_resnet_trunk_split")
+
+    def mfma_flops_per_row(self) -> int:
+        """FLOPs the split trunk kernel executes on the bf16 matrix cores per board: six partial
+        products per fp32 product, stem K padded 27 -> 32."""
+        cells, f = self.board_size ** 2, self.filters
+        return 6 * 2 * cells * f * (32 + 2 * self.n_blocks * 9 * f)
+
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
         if self.use_resnet:

@@ -59,8 +59,8 @@ def parse():
     ap.add_argument("--board", type=int, default=None)
     ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--nn-kernel", choices=["auto", "resnet", "miopen"], default="auto",
-                    help="leaf evaluator: rvz_resnet_fwd_f32 (fused fp32 MFMA) or MIOpen convs")
+    ap.add_argument("--nn-kernel", choices=["auto", "split", "resnet", "miopen"], default="auto",
+                    help="leaf evaluator: split (fp32 as exact 3xbf16 split, MFMA), resnet (f32 MFMA), miopen")
     ap.add_argument("--instrument-plies", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -89,6 +89,7 @@ def instrumented(run, eng, ev, plies):
     and the intervals bracket only the kernels. The NN is timed separately (back-to-back calls)."""
     eng.stats_enable(True)
     eng.timing_enable(True)
+    nn_calls = 0
     for _ in range(plies):
         torch.cuda.synchronize(eng.device)
         torch.cuda._sleep(int(60e6))        # ~25-30 ms of device time: the host enqueues meanwhile
@@ -96,6 +97,7 @@ def instrumented(run, eng, ev, plies):
         while eng.search_step():
             logits, value = ev(eng.leaf_x)
             eng.search_submit(logits, value, True)
+            nn_calls += 1
         eng.act(run.temperature, apply=True)
         run.restart_finished(eng.get_state()[2])
     t = eng.timing_read()
@@ -112,7 +114,15 @@ def instrumented(run, eng, ev, plies):
     b.record(stream)
     torch.cuda.synchronize(eng.device)
     ms = {"step": t["step"][0], "act": t["act"][0], "nn": a.elapsed_time(b) / 10}
-    n = {"step": t["step"][1], "act": t["act"][1]}
+    n = {"step": t["step"][1], "act": t["act"][1], "nn": nn_calls}
+    if getattr(ev, "kernel", None) == "split":   # the trunk launch alone: the dominant kernel
+        ev.trunk_only(eng.leaf_x)
+        a.record(stream)
+        for _ in range(10):
+            ev.trunk_only(eng.leaf_x)
+        b.record(stream)
+        torch.cuda.synchronize(eng.device)
+        ms["nn_trunk"] = a.elapsed_time(b) / 10
     return ms, n, {"step": st, "act": act}
 
 
@@ -220,14 +230,36 @@ def main():
                       "achieved_GBs": per_launch / (ms[k] * 1e-3) / 1e9}
     dom = max(("step", "act"),
               key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
-    traffic = None
+    pmc = {}
     if os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096:
         try:
-            traffic = json.load(open(args.pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+            pmc = json.load(open(args.pmc))
         except Exception:
-            traffic = None
+            pmc = {}
+    traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
     nn_flops = ev.flops_per_row() * args.games
     nn_tflops = nn_flops / (ms["nn"] * 1e-3) / 1e12
+    nn_per_ply = n["nn"] / max(1, args.instrument_plies)
+    split = "nn_trunk" in ms
+    if split:   # roofline of the NN trunk kernel: executed bf16-MFMA FLOPs per launch / duration
+        mf = ev.mfma_flops_per_row() * args.games
+        nn_roof = {"kernel": "k_resnet_split", "bound": "mfma",
+                   "achieved": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12, 2),
+                   "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
+                   "frac": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
+                   "traffic": pmc.get("nn_trunk", {}).get("hbm_bytes_per_launch"),
+                   "avg_ms_per_launch": round(ms["nn_trunk"], 4),
+                   "mfma_flops_per_launch": mf,
+                   "fp32_equiv_tflops": round(nn_flops / (ms["nn_trunk"] * 1e-3) / 1e12, 2)}
+    else:
+        nn_roof = {"kernel": "rvz_resnet_fwd_f32" if ev.use_resnet else "miopen",
+                   "bound": "mfma", "achieved": round(nn_tflops, 2),
+                   "peak": MFMA_PEAK_TFLOPS[args.nn_dtype], "unit": "TFLOP/s",
+                   "frac": round(nn_tflops / MFMA_PEAK_TFLOPS[args.nn_dtype], 4), "traffic": None}
+    nn_roof["avg_ms_per_call"] = round(ms["nn"], 4)
+    nn_roof["calls_per_ply"] = round(nn_per_ply, 2)
+    search_ms_per_ply = kernels[dom]["avg_us"] * kernels[dom]["launches_per_ply"] / 1e3
+    nn_dominant = ms.get("nn_trunk", ms["nn"]) * nn_per_ply > search_ms_per_ply
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -235,6 +267,9 @@ def main():
 
     if rank == 0:
         ach = kernels[dom]["achieved_GBs"]
+        search_roof = {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(ach, 2),
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic}
         out = {
             "metric": f"self-play board-steps/sec @ {args.sims} sims/move, "
                       f"{args.board}x{args.board} Reversi",
@@ -242,22 +277,22 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u64+f32", "data": "synthetic (start position, per-game seeds, random-init net)",
+            "dtype": "u64 rules + f32 NN" + (" (exact 3xbf16 split on MFMA)" if split else ""),
+            "data": "synthetic (start position, per-game seeds, random-init net)",
             "config": {"workload": f"{args.config}: {args.games} games/GPU x {args.sims} sims, "
                                    f"{args.blocks}x{args.filters} ResNet, {args.board}x{args.board}",
                        "games_per_gpu": args.games, "global_games": args.games * world,
                        "sims": args.sims, "batch": args.batch,
                        "nn": f"{args.blocks}x{args.filters}", "nn_dtype": args.nn_dtype,
-                       "nn_kernel": "rvz_resnet_fwd_f32" if ev.use_resnet else "miopen+rvz_nn_bias_act",
+                       "nn_kernel": {"split": "rvz_resnet_fwd_split", "resnet": "rvz_resnet_fwd_f32"}
+                       .get(getattr(ev, "kernel", ""), "miopen+rvz_nn_bias_act"),
                        "graph": not args.no_graph, "parallelism": f"games sharded x{world}"},
-            "roofline": {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(ach, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic},
+            # the dominant kernel of a ply (by time per ply) carries "roofline"; the other side
+            # of the ply (NN vs search) is reported beside it
+            "roofline": nn_roof if nn_dominant else search_roof,
+            "search_roofline" if nn_dominant else "nn_roofline":
+                search_roof if nn_dominant else nn_roof,
             "kernels": {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()},
-            "nn_roofline": {"bound": "mfma", "achieved": round(nn_tflops, 2),
-                            "peak": MFMA_PEAK_TFLOPS[args.nn_dtype], "unit": "TFLOP/s",
-                            "frac": round(nn_tflops / MFMA_PEAK_TFLOPS[args.nn_dtype], 4),
-                            "avg_ms_per_call": round(ms["nn"], 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

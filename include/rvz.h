@@ -162,6 +162,13 @@ int64_t rvz_resnet_work_size(int32_t n);
 int rvz_resnet_fwd_split(const float *x, int32_t n, const float *params, const uint16_t *wsplit,
                          int32_t filters, int32_t blocks, float *work, float *logits,
                          float *value, void *hip_stream);
+/* rvz_resnet_fwd_split's two launches on their own: the trunk (stem, residual tower, 1x1 head
+ * convs -> work) and the batched FC heads (work -> logits, value). */
+int rvz_resnet_trunk_split(const float *x, int32_t n, const float *params,
+                           const uint16_t *wsplit, int32_t filters, int32_t blocks, float *work,
+                           void *hip_stream);
+int rvz_resnet_heads_fc(const float *work, int32_t n, const float *params, int32_t filters,
+                        int32_t blocks, float *logits, float *value, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,69 @@
+"""A/B timing of compile-time variants of the split ResNet kernel in ONE process (same box, same
+clock state): each variant is a private build of csrc/rvz_resnet.hip with extra -D flags; the
+variants are timed alternately (A B A B ...) so drift cancels.
+
+    RVZ_AB='base:;stem0:-DRVZ_STEM_MFMA=0' python tools/ab_split.py [blocks filters n]
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "alphazero-reversi_amd"))
+import rvz  # noqa: E402
+from rvz import _lib  # noqa: E402
+
+src = os.path.join(ROOT, "alphazero-reversi_amd", "csrc", "rvz_resnet.hip")
+variants = []
+for item in os.environ.get("RVZ_AB", "base:").split(";"):
+    name, flags = item.split(":", 1)
+    so = f"/tmp/librvz_ab_{name}.so"
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                           "-fPIC", "-ffp-contract=off", "-fno-gpu-flush-denormals-to-zero",
+                           *flags.split(), "-shared", "-o", so, src])
+    variants.append((name, C.CDLL(so)))
+
+blocks, filters, n = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (6, 64, 4096)))
+torch.manual_seed(0)
+net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
+ev = rvz.LeafEvaluator(net, kernel="split")
+x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
+lg = torch.empty(n, 65, device="cuda")
+v = torch.empty(n, device="cuda")
+wk = torch.empty(n * 192, device="cuda")
+ref_l, ref_v = ev(x)
+ref_l, ref_v = ref_l.clone(), ref_v.clone()
+s = _lib.stream_handle()
+
+
+def run(lib):
+    rc = lib.rvz_resnet_fwd_split(C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
+                                  C.c_void_p(ev.wsplit.data_ptr()), filters, blocks,
+                                  C.c_void_p(wk.data_ptr()), C.c_void_p(lg.data_ptr()),
+                                  C.c_void_p(v.data_ptr()), C.c_void_p(s))
+    assert rc == 0
+
+
+res = {name: [] for name, _ in variants}
+err = {}
+for name, lib in variants:
+    run(lib)
+    torch.cuda.synchronize()
+    err[name] = max((lg - ref_l).abs().max().item(), (v - ref_v).abs().max().item())
+for rep in range(5):
+    for name, lib in variants:
+        for _ in range(3):
+            run(lib)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(20):
+            run(lib)
+        b.record()
+        torch.cuda.synchronize()
+        res[name].append(a.elapsed_time(b) / 20)
+print(json.dumps({name: {"ms_min": round(min(t), 4), "ms_med": round(sorted(t)[2], 4),
+                         "max_abs_diff_vs_default": err[name]} for name, t in res.items()}))

@@ -17,7 +17,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"step": "k_step<", "act": "k_act<", "expand_backup": "k_expand_backup<",
-           "reset": "k_reset<", "nn_conv3x3": "igemm_fwd_gtcx35_nhwc_fp32_bx0_ex1_bt128x64x16"}
+           "reset": "k_reset<", "nn_trunk": "k_resnet_split<", "nn_heads": "k_heads_fc(",
+           "nn_conv3x3": "igemm_fwd_gtcx35_nhwc_fp32_bx0_ex1_bt128x64x16"}
 
 
 def load(run_dir, counter):
