@@ -522,38 +522,80 @@ __global__ __launch_bounds__(256, 2) void k_resnet_fwd(const float* __restrict__
 
 #ifdef RVZ_PHASE_TIMING   // tools/phase_timing.py: per-workgroup s_memtime at phase boundaries
 __device__ uint64_t g_phase[65536][8];
+__device__ uint64_t g_rt[65536][2];   // s_memrealtime (100 MHz) at start / end
 __device__ uint64_t g_wave[65536][16];
 #define PHASE(i) \
     if (threadIdx.x == 0 && blockIdx.x < 65536) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
+#define RT(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_rt[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
 #define WAVE_T(i) \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 65536) \
         g_wave[blockIdx.x][(threadIdx.x >> 6) + 8 * (i)] = __builtin_amdgcn_s_memtime()
 #else
 #define PHASE(i)
 #define WAVE_T(i)
+#define RT(i)
 #endif
 
-template <int F, int NBOARD>
+// MFMA shape traits (D = W X^T: TM output channels x TN pixels, K input channels per step)
+struct Shape32 {   // v_mfma_f32_32x32x16_bf16
+    static constexpr int TM = 32, TN = 32, K = 16, NG = 4;
+    typedef f32x16 acc_t;
+    // channel offset (within the tile) of register group g; registers 4g .. 4g+3
+    static __device__ __forceinline__ int chan(int g, int lane) { return 8 * g + 4 * (lane >> 5); }
+    static __device__ __forceinline__ acc_t mfma(bf16x8 a, bf16x8 b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    }
+};
+struct Shape16 {   // v_mfma_f32_16x16x32_bf16
+    static constexpr int TM = 16, TN = 16, K = 32, NG = 1;
+    typedef f32x4 acc_t;
+    static __device__ __forceinline__ int chan(int, int lane) { return 4 * (lane >> 4); }
+    static __device__ __forceinline__ acc_t mfma(bf16x8 a, bf16x8 b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+
+// 16x16x32 by default: on random data the chip holds a higher clock on it than on 32x32x16
+// (MI355X_MICROARCH.md 'DVFS give-back' item 7); measured 0.875 vs 0.942 ms per C2 leaf batch
+#ifndef RVZ_SPLIT_SHAPE
+#define RVZ_SPLIT_SHAPE 16
+#endif
+#if RVZ_SPLIT_SHAPE == 16
+typedef Shape16 SplitShape;
+#ifndef RVZ_SPLIT_CTW
+#define RVZ_SPLIT_CTW 2      // channel tiles per wave
+#define RVZ_SPLIT_PTW 4      // pixel tiles per wave
+#endif
+#else
+typedef Shape32 SplitShape;
+#ifndef RVZ_SPLIT_CTW
+#define RVZ_SPLIT_CTW 1
+#define RVZ_SPLIT_PTW 2
+#endif
+#endif
+
+template <class S, int F, int NBOARD>
 struct CfgS {
-    static constexpr int CSB = F + 8;                // bf16 per pixel row
+    // a row is F + PAD bf16 = R 16-byte slots. ds_read_b128 lane groups are {0-3,12-15,20-27},
+    // {4-11,16-19,28-31} (+32). 32x32x16: a half-wave reads 32 consecutive pixels at one
+    // k-offset, every group holds all 16 pixel residues mod 16 -> R odd is conflict-free.
+    // 16x16x32: a group holds pixels {0-3,12-15} at k-offset q and {4-11} at q+1 -> R = 2 mod 4.
+    static constexpr int CSB = S::TM == 32 ? F + 8 : F + 16;   // bf16 per pixel row
     static constexpr int ZROW = NBOARD * 64;         // the zero row
     static constexpr int PLANE = (ZROW + 1) * CSB;   // bf16 per part
     static constexpr int ACT = 3 * PLANE;            // bf16 per buffer
     static constexpr int XIN = NBOARD * 100 * 4;     // floats
     static constexpr int BYTES = 2 * ACT * 2 + 4 * XIN;
-    static constexpr int KS = F / 16;                // k-steps per tap
+    static constexpr int KS = F / S::K;              // k-steps per tap
     static constexpr int NIT = 9 * KS;               // k-steps per layer
-    static constexpr int CT = F / 32;                // channel tiles
-    static constexpr int PT = NBOARD * 2;            // pixel tiles
-    static_assert(CT * PT == 8, "8 waves, one 32x32 tile each");
-    static_assert((CSB * 2 / 16) % 2 == 1, "odd number of 16-byte slots per row");
+    static constexpr int CT = F / S::TM;             // channel tiles
+    static_assert(S::TM == 32 ? (CSB * 2 / 16) % 2 == 1 : (CSB * 2 / 16) % 4 == 2,
+                  "conflict-free row stride");
     static_assert((PLANE * 2) % 16 == 0, "16-byte aligned parts");
     static_assert(BYTES <= 160 * 1024, "fits the 160 KiB LDS of a CU");
 };
 
-#ifndef RVZ_SPLIT_TPW
-#define RVZ_SPLIT_TPW 2      // 32x32 tiles per wave
-#endif
 #ifndef RVZ_SPLIT_PD
 #define RVZ_SPLIT_PD 3       // weight prefetch distance, k-steps
 #endif
@@ -567,52 +609,70 @@ struct CfgS {
 static_assert(RVZ_SPLIT_PD <= RVZ_SPLIT_PAD, "prefetch stays inside the padded buffer");
 
 __host__ __device__ inline int64_t split_layer_elems(int F) { return (int64_t)9 * F * F * 3; }
-__host__ __device__ inline int64_t split_kstep_elems(int F) { return (int64_t)3 * F * 16; }
+__host__ __device__ inline int64_t split_kstep_elems(int F) {   // one k-step, all parts/tiles
+    return (int64_t)3 * F * SplitShape::K;
+}
+
+// the wave's tiles: CTW channel tiles x PTW pixel tiles
+template <class S, int F, int CTW, int PTW>
+struct WaveTiles {
+    static constexpr int CG = F / (CTW * S::TM);     // channel groups (waves along channels)
+    int ct0, px[PTW];
+    __device__ WaveTiles(int wave, int lane) {
+        ct0 = (wave % CG) * CTW;
+        const int pt0 = (wave / CG) * PTW;
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) px[u] = (pt0 + u) * S::TN + lane % S::TN;
+    }
+};
 
 // conv epilogue: bias (+ skip), ReLU, exact split back into the three parts; per register group
-// g the lane holds channels ct*32 + 8g + 4h .. +3 of its pixel -> 8-byte reads/writes
-template <int F, int NBOARD, int TPW, bool RES>
-__device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out, const f32x16 (&hi)[TPW],
-                                               const f32x16 (&lo)[TPW],
-                                               const float* __restrict__ bias, int ct,
-                                               const int (&px)[TPW], int h) {
-    using C = CfgS<F, NBOARD>;
+// g of tile (c, u) the lane holds 4 consecutive channels of its pixel -> 8-byte reads/writes
+template <class S, int F, int NBOARD, int CTW, int PTW, bool RES>
+__device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out,
+                                               const typename S::acc_t (&hi)[CTW][PTW],
+                                               const typename S::acc_t (&lo)[CTW][PTW],
+                                               const float* __restrict__ bias,
+                                               const WaveTiles<S, F, CTW, PTW>& wt, int lane) {
+    using C = CfgS<S, F, NBOARD>;
     typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int u = 0; u < TPW; ++u)
+    for (int c = 0; c < CTW; ++c)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int n0 = ct * 32 + 8 * g + 4 * h;
-            const f32x4 bn = *reinterpret_cast<const f32x4*>(bias + n0);
-            uint16_t* o = out + px[u] * C::CSB + n0;
-            u16x4 s0, s1, s2;
-            if (RES) {
-                s0 = *reinterpret_cast<const u16x4*>(o);
-                s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
-                s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
-            }
-            u32x2 d0, d1, d2;
+        for (int u = 0; u < PTW; ++u)
 #pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                f32x2 v;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int j = 2 * hf + e, reg = 4 * g + j;
-                    v[e] = (hi[u][reg] + lo[u][reg]) + bn[j];
-                    if (RES) v[e] += join3(s0[j], s1[j], s2[j]);   // skip input, in place
-                    v[e] = fmaxf(v[e], 0.0f);
+            for (int g = 0; g < S::NG; ++g) {
+                const int n0 = (wt.ct0 + c) * S::TM + S::chan(g, lane);
+                const f32x4 bn = *reinterpret_cast<const f32x4*>(bias + n0);
+                uint16_t* o = out + wt.px[u] * C::CSB + n0;
+                u16x4 s0, s1, s2;
+                if (RES) {
+                    s0 = *reinterpret_cast<const u16x4*>(o);
+                    s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
+                    s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
                 }
-                uint32_t h0, h1, h2;
-                split3x2(v, h0, h1, h2);
-                d0[hf] = h0;
-                d1[hf] = h1;
-                d2[hf] = h2;
+                u32x2 d0, d1, d2;
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    f32x2 v;
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int j = 2 * hf + e, reg = 4 * g + j;
+                        v[e] = (hi[c][u][reg] + lo[c][u][reg]) + bn[j];
+                        if (RES) v[e] += join3(s0[j], s1[j], s2[j]);   // skip input, in place
+                        v[e] = fmaxf(v[e], 0.0f);
+                    }
+                    uint32_t h0, h1, h2;
+                    split3x2(v, h0, h1, h2);
+                    d0[hf] = h0;
+                    d1[hf] = h1;
+                    d2[hf] = h2;
+                }
+                *reinterpret_cast<u32x2*>(o) = d0;
+                *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
+                *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
             }
-            *reinterpret_cast<u32x2*>(o) = d0;
-            *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
-            *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
-        }
 }
 
 // 8 bf16 parts p of 8 fp32 values
@@ -632,131 +692,150 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&out)[3]) {
     out[2] = __builtin_bit_cast(bf16x8, w2);
 }
 
+// the six partial products: (weight part, activation part), hi first
+__device__ constexpr int kTW[6] = {0, 0, 2, 1, 0, 1};
+__device__ constexpr int kTA[6] = {0, 2, 0, 1, 1, 0};
+
 // stem conv 3 -> F (network.py:33-34 + BN folded) as a K = 27 (padded to 32) GEMM on the same
 // split MFMA and tile map as the trunk: k = tap*3 + ch; A = stem weights (split in registers),
 // B = the input taps read from the halo-padded xin; epilogue into actA.
-template <int F, int NBOARD, int TPW>
+template <class S, int F, int NBOARD, int CTW, int PTW>
 __device__ __forceinline__ void stem_split(const float* xin, uint16_t* __restrict__ out,
                                            const float* __restrict__ prm, const Layout& L,
                                            int wave, int lane) {
-    using C = CfgS<F, NBOARD>;
-    constexpr int CT = C::CT;
-    const int ct = wave % CT, pt0 = (wave / CT) * TPW;
-    const int m = lane & 31, h = lane >> 5;
-    int px[TPW];
+    const WaveTiles<S, F, CTW, PTW> wt(wave, lane);
+    const int kq = 8 * (lane / S::TM);               // this lane's k offset in a step
+    typename S::acc_t hi[CTW][PTW], lo[CTW][PTW];
 #pragma unroll
-    for (int u = 0; u < TPW; ++u) px[u] = (pt0 + u) * 32 + m;
-    f32x16 hi[TPW], lo[TPW];
+    for (int c = 0; c < CTW; ++c)
 #pragma unroll
-    for (int u = 0; u < TPW; ++u) {
-        hi[u] = f32x16{};
-        lo[u] = f32x16{};
-    }
-    const float* wrow = prm + L.stem_w + (ct * 32 + m) * 27;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-        float wv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = ks * 16 + 8 * h + j;
-            wv[j] = k < 27 ? wrow[k] : 0.0f;
+        for (int u = 0; u < PTW; ++u) {
+            hi[c][u] = typename S::acc_t{};
+            lo[c][u] = typename S::acc_t{};
         }
-        bf16x8 wq[3];
-        split8(wv, wq);
 #pragma unroll
-        for (int u = 0; u < TPW; ++u) {
-            const int b = px[u] >> 6, r = (px[u] & 63) >> 3, c = px[u] & 7;
+    for (int ks = 0; ks < 32 / S::K; ++ks) {
+        bf16x8 wq[CTW][3], aq[PTW][3];
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) {
+            const float* wrow = prm + L.stem_w + ((wt.ct0 + c) * S::TM + lane % S::TM) * 27;
+            float wv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = ks * S::K + kq + j;
+                wv[j] = k < 27 ? wrow[k] : 0.0f;
+            }
+            split8(wv, wq[c]);
+        }
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) {
+            const int px = wt.px[u], b = px >> 6, r = (px & 63) >> 3, cc = px & 7;
             float xv[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int k = ks * 16 + 8 * h + j, t = k / 3, ch = k % 3;
-                xv[j] = k < 27 ? xin[(b * 100 + (r + t / 3) * 10 + (c + t % 3)) * 4 + ch] : 0.0f;
+                const int k = ks * S::K + kq + j, t = k / 3, ch = k % 3;
+                xv[j] = k < 27 ? xin[(b * 100 + (r + t / 3) * 10 + (cc + t % 3)) * 4 + ch] : 0.0f;
             }
-            bf16x8 aq[3];
-            split8(xv, aq);
-            constexpr int TW[6] = {0, 0, 2, 1, 0, 1}, TA[6] = {0, 2, 0, 1, 1, 0};
-#pragma unroll
-            for (int term = 0; term < 6; ++term) {
-                f32x16& acc = term == 0 ? hi[u] : lo[u];
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wq[TW[term]], aq[TA[term]], acc, 0,
-                                                              0, 0);
-            }
+            split8(xv, aq[u]);
         }
+#pragma unroll
+        for (int term = 0; term < 6; ++term)
+#pragma unroll
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int u = 0; u < PTW; ++u) {
+                    auto& acc = term == 0 ? hi[c][u] : lo[c][u];
+                    acc = S::mfma(wq[c][kTW[term]], aq[u][kTA[term]], acc);
+                }
     }
-    epilogue_split<F, NBOARD, TPW, false>(out, hi, lo, prm + L.stem_b, ct, px, h);
+    epilogue_split<S, F, NBOARD, CTW, PTW, false>(out, hi, lo, prm + L.stem_b, wt, lane);
 }
 
-template <int F, int NBOARD, int TPW, bool RES>
+// sched_group_barrier pattern: NM MFMAs, the first ND gaps get one LDS read, the next NV one
+// global load
+template <int I, int NM, int ND, int NV>
+__device__ __forceinline__ void interleave_loads() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if constexpr (I < ND) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    else if constexpr (I < ND + NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    if constexpr (I + 1 < NM) interleave_loads<I + 1, NM, ND, NV>();
+}
+
+template <class S, int F, int NBOARD, int CTW, int PTW, bool RES>
 __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
                                            uint16_t* __restrict__ out,
                                            const uint16_t* __restrict__ wl,   // layer fragments
                                            const float* __restrict__ bias, int wave, int lane,
-                                           bf16x8 (&bc)[RVZ_SPLIT_PD][3], int ptag = -1) {
-    using C = CfgS<F, NBOARD>;
+                                           bf16x8 (&bc)[RVZ_SPLIT_PD][CTW][3], int ptag = -1) {
+    using C = CfgS<S, F, NBOARD>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_SPLIT_PD;
-    const int ct = wave % CT, pt0 = (wave / CT) * TPW;   // channel tile, first pixel tile
-    const int m = lane & 31, h = lane >> 5;
-    // this lane's pixel in each of the wave's pixel tiles, and the taps that stay on its board
-    int px[TPW];
-    unsigned pmask[TPW];
+    const WaveTiles<S, F, CTW, PTW> wt(wave, lane);
+    const int kq = 8 * (lane / S::TM);
+    // the taps of each of the lane's pixels that stay on its board
+    unsigned pmask[PTW];
 #pragma unroll
-    for (int u = 0; u < TPW; ++u) {
-        px[u] = (pt0 + u) * 32 + m;
-        const int rr = (px[u] & 63) >> 3, cc = px[u] & 7;
+    for (int u = 0; u < PTW; ++u) {
+        const int rr = (wt.px[u] & 63) >> 3, cc = wt.px[u] & 7;
         unsigned msk = 0;
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             if ((unsigned)(rr + t / 3 - 1) < 8u && (unsigned)(cc + t % 3 - 1) < 8u) msk |= 1u << t;
         pmask[u] = msk;
     }
-    f32x16 hi[TPW], lo[TPW];
+    typename S::acc_t hi[CTW][PTW], lo[CTW][PTW];
 #pragma unroll
-    for (int u = 0; u < TPW; ++u) {
-        hi[u] = f32x16{};
-        lo[u] = f32x16{};
-    }
-    // fragment (it, part) of this lane: wf[(it*3 + part)*CT*64]
-    const bf16x8* wf = reinterpret_cast<const bf16x8*>(wl) + ct * 64 + lane;
-    auto load_b = [&](bf16x8 (&bq)[3], int it) {
+    for (int c = 0; c < CTW; ++c)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bq[p] = wf[(it * 3 + p) * CT * 64];
+        for (int u = 0; u < PTW; ++u) {
+            hi[c][u] = typename S::acc_t{};
+            lo[c][u] = typename S::acc_t{};
+        }
+    // fragment (it, part, ctile) of this lane: wf[((it*3 + part)*CT + ctile)*64]
+    const bf16x8* wf = reinterpret_cast<const bf16x8*>(wl) + wt.ct0 * 64 + lane;
+    auto load_b = [&](bf16x8 (&bq)[CTW][3], int it) {
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bq[c][p] = wf[((it * 3 + p) * CT + c) * 64];
     };
-    auto load_a = [&](bf16x8 (&aq)[TPW][3], int it) {
+    auto load_a = [&](bf16x8 (&aq)[PTW][3], int it) {
         const int t = it / KS, ks = it - t * KS;
         const int off = (t / 3 - 1) * 8 + (t % 3 - 1);
 #pragma unroll
-        for (int u = 0; u < TPW; ++u) {
-            const int row = (pmask[u] >> t) & 1u ? px[u] + off : C::ZROW;
-            const uint16_t* ap = in + row * C::CSB + ks * 16 + 8 * h;
+        for (int u = 0; u < PTW; ++u) {
+            const int row = (pmask[u] >> t) & 1u ? wt.px[u] + off : C::ZROW;
+            const uint16_t* ap = in + row * C::CSB + ks * S::K + kq;
 #pragma unroll
             for (int p = 0; p < 3; ++p)
                 aq[u][p] = *reinterpret_cast<const bf16x8*>(ap + p * C::PLANE);
         }
     };
-    // (weight part, activation part) of the six products, hi first; tiles interleaved so that
     // consecutive MFMAs of one wave go to different accumulators
-    constexpr int TW[6] = {0, 0, 2, 1, 0, 1}, TA[6] = {0, 2, 0, 1, 1, 0};
-    auto compute = [&](const bf16x8 (&aq)[TPW][3], const bf16x8 (&bq)[3]) {
+    auto compute = [&](const bf16x8 (&aq)[PTW][3], const bf16x8 (&bq)[CTW][3]) {
 #pragma unroll
         for (int term = 0; term < 6; ++term)
 #pragma unroll
-            for (int u = 0; u < TPW; ++u) {
-                f32x16& acc = term == 0 ? hi[u] : lo[u];
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bq[TW[term]], aq[u][TA[term]], acc,
-                                                              0, 0, 0);
-            }
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int u = 0; u < PTW; ++u) {
+                    auto& acc = term == 0 ? hi[c][u] : lo[c][u];
+                    acc = S::mfma(bq[c][kTW[term]], aq[u][kTA[term]], acc);
+                }
     };
     // Software pipeline, fully unrolled (constant register indices, no copies of in-flight
-    // loads): step it computes while step it+1's activation fragments (LDS) and step it+PD's
-    // weight fragments (L2) load; sched_barrier keeps the scheduler from sinking the loads next
-    // to their use. bc carries the next layer's first PD k-steps (layers are contiguous; the
-    // buffer has RVZ_SPLIT_PAD k-steps of padding after the last).
-    bf16x8 bq[NIT + PD][3];
-    bf16x8 aq[3][TPW][3];                 // activation fragments, two k-steps ahead
+    // loads): step it computes while step it+2's activation fragments (LDS) and step it+PD's
+    // weight fragments (L2) load, one load per MFMA issue gap (an MFMA leaves most of its issue
+    // cycles free; 9+ loads back to back would let the matrix pipe drain). bc carries the next
+    // layer's first PD k-steps (layers are contiguous; the buffer has RVZ_SPLIT_PAD k-steps of
+    // padding after the last).
+    bf16x8 bq[NIT + PD][CTW][3];
+    bf16x8 aq[3][PTW][3];
 #pragma unroll
     for (int d = 0; d < PD; ++d)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bq[d][p] = bc[d][p];
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bq[d][c][p] = bc[d][c][p];
     load_a(aq[0], 0);
     load_a(aq[1], 1);
 #pragma unroll
@@ -765,18 +844,7 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
         load_b(bq[it + PD], it + PD);
 #if RVZ_SPLIT_INTERLEAVE
         compute(aq[it % 3], bq[it]);
-        if constexpr (TPW == 2) {
-            // one load per MFMA issue gap (an MFMA leaves 24 of its 32 cycles free), instead of
-            // 9 loads back to back while the matrix pipe drains
-#define RVZ_SGB(mask) __builtin_amdgcn_sched_group_barrier(mask, 1, 0)
-            RVZ_SGB(0x008); RVZ_SGB(0x100); RVZ_SGB(0x008); RVZ_SGB(0x100);
-            RVZ_SGB(0x008); RVZ_SGB(0x100); RVZ_SGB(0x008); RVZ_SGB(0x100);
-            RVZ_SGB(0x008); RVZ_SGB(0x100); RVZ_SGB(0x008); RVZ_SGB(0x100);
-            RVZ_SGB(0x008); RVZ_SGB(0x020); RVZ_SGB(0x008); RVZ_SGB(0x020);
-            RVZ_SGB(0x008); RVZ_SGB(0x020); RVZ_SGB(0x008); RVZ_SGB(0x008);
-            RVZ_SGB(0x008); RVZ_SGB(0x008);
-#undef RVZ_SGB
-        }
+        interleave_loads<0, 6 * CTW * PTW, 3 * PTW, 3 * CTW>();
         __builtin_amdgcn_sched_barrier(0);
 #else
         __builtin_amdgcn_sched_barrier(0);
@@ -787,26 +855,27 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
 #pragma unroll
     for (int d = 0; d < PD; ++d)
 #pragma unroll
-        for (int p = 0; p < 3; ++p) bc[d][p] = bq[NIT + d][p];
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bc[d][c][p] = bq[NIT + d][c][p];
     if (ptag >= 0) {
         PHASE(ptag);
         WAVE_T(0);
     }
-    epilogue_split<F, NBOARD, TPW, RES>(out, hi, lo, bias, ct, px, h);
+    epilogue_split<S, F, NBOARD, CTW, PTW, RES>(out, hi, lo, bias, wt, lane);
 }
 
-// TPW = 32x32 output tiles per wave: 1 -> 8 waves (two per SIMD), 2 -> 4 waves (one per SIMD,
-// each weight fragment reused over two pixel tiles)
-template <int F, int NBOARD, int TPW>
-__global__ __launch_bounds__(512 / TPW, 1) void k_resnet_split(const float* __restrict__ x,
-                                                               int n_boards,
-                                                               const float* __restrict__ prm,
-                                                               Layout L,
-                                                               const uint16_t* __restrict__ wsp,
-                                                               int n_blocks,
-                                                               float* __restrict__ work) {
-    using C = CfgS<F, NBOARD>;
-    constexpr int NTHR = 512 / TPW;
+// one workgroup = 4 waves (one per SIMD) = NBOARD boards; wave tile CTW x PTW MFMA tiles
+template <class S, int F, int NBOARD, int CTW, int PTW>
+__global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict__ x,
+                                                         int n_boards,
+                                                         const float* __restrict__ prm, Layout L,
+                                                         const uint16_t* __restrict__ wsp,
+                                                         int n_blocks, float* __restrict__ work) {
+    using C = CfgS<S, F, NBOARD>;
+    using WT = WaveTiles<S, F, CTW, PTW>;
+    static_assert(WT::CG * (NBOARD * 64 / (PTW * S::TN)) == 4, "4 waves");
+    constexpr int NTHR = 256;
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
     uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
     uint16_t* actB = actA + C::ACT;
@@ -815,6 +884,7 @@ __global__ __launch_bounds__(512 / TPW, 1) void k_resnet_split(const float* __re
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = blockIdx.x * NBOARD;
     PHASE(0);
+    RT(0);
 
     // zero rows of both buffers, all parts (6 consecutive planes)
     for (int i = tid; i < 6 * C::CSB; i += NTHR) {
@@ -822,19 +892,21 @@ __global__ __launch_bounds__(512 / TPW, 1) void k_resnet_split(const float* __re
         actA[part * C::PLANE + C::ZROW * C::CSB + k] = 0;
     }
     // the first PD k-steps' weight fragments, in flight during the input and stem
-    bf16x8 bc[RVZ_SPLIT_PD][3];
+    bf16x8 bc[RVZ_SPLIT_PD][CTW][3];
     if (n_blocks > 0) {
-        const bf16x8* wf = reinterpret_cast<const bf16x8*>(wsp) + (wave % C::CT) * 64 + lane;
+        const bf16x8* wf = reinterpret_cast<const bf16x8*>(wsp) + WT(wave, lane).ct0 * 64 + lane;
 #pragma unroll
         for (int s = 0; s < RVZ_SPLIT_PD; ++s)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bc[s][p] = wf[(s * 3 + p) * C::CT * 64];
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) bc[s][c][p] = wf[((s * 3 + p) * C::CT + c) * 64];
     }
     load_input<NBOARD>(x, n_boards, g0, xin, tid, NTHR);
     __syncthreads();
     const ActSplit outA{actA, C::CSB, C::PLANE};
 #if RVZ_STEM_MFMA
-    stem_split<F, NBOARD, TPW>(xin, actA, prm, L, wave, lane);
+    stem_split<S, F, NBOARD, CTW, PTW>(xin, actA, prm, L, wave, lane);
 #else
     stem<F, NBOARD, NTHR>(xin, outA, prm, L, tid);
 #endif
@@ -843,35 +915,38 @@ __global__ __launch_bounds__(512 / TPW, 1) void k_resnet_split(const float* __re
     const int64_t LW = split_layer_elems(F);
     for (int blk = 0; blk < n_blocks; ++blk) {
         const int l1 = 2 * blk, l2 = 2 * blk + 1;
-        conv_split<F, NBOARD, TPW, false>(actA, actB, wsp + l1 * LW,
-                                          prm + L.res_b + (size_t)l1 * F, wave, lane, bc,
-                                          blk == 0 ? 4 : -1);
+        conv_split<S, F, NBOARD, CTW, PTW, false>(actA, actB, wsp + l1 * LW,
+                                                  prm + L.res_b + (size_t)l1 * F, wave, lane, bc,
+                                                  blk == 0 ? 4 : -1);
         if (blk == 0) {
             PHASE(5);
             WAVE_T(1);
         }
         __syncthreads();
         if (blk == 0) PHASE(6);
-        conv_split<F, NBOARD, TPW, true>(actB, actA, wsp + l2 * LW,
-                                         prm + L.res_b + (size_t)l2 * F, wave, lane, bc);
+        conv_split<S, F, NBOARD, CTW, PTW, true>(actB, actA, wsp + l2 * LW,
+                                                 prm + L.res_b + (size_t)l2 * F, wave, lane, bc);
         __syncthreads();
     }
     PHASE(2);
     head_convs<F, NBOARD, NTHR>(outA, reinterpret_cast<float*>(actB), prm, L,
                                 HeadsGlobal{work, g0, n_boards}, tid);
     PHASE(3);
+    RT(1);
 }
 
-// res_w[l][t][n][k] fp32 -> frag[l][t][ks][part][ctile][lane][8] bf16 parts
+// res_w[l][t][n][k] fp32 -> frag[l][t][ks][part][ctile][lane][8] bf16 parts, for SplitShape:
+// lane = ((k % K) / 8) * TM + n % TM (the A-operand lane map)
 __global__ void k_split_weights(const float* __restrict__ w, int F, int64_t total,
                                 uint16_t* __restrict__ out) {
-    const int KS = F / 16, CT = F / 32;
+    constexpr int K = SplitShape::K, TM = SplitShape::TM;
+    const int KS = F / K, CT = F / TM;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int k = (int)(i % F), n = (int)((i / F) % F);
         const int64_t lt = i / ((int64_t)F * F);             // layer*9 + tap
-        const int ks = k / 16, hh = (k % 16) / 8, j = k % 8, ct = n / 32, mm = n % 32;
-        const int ln = hh * 32 + mm;
+        const int ks = k / K, j = k % 8, ct = n / TM;
+        const int ln = ((k % K) / 8) * TM + n % TM;
         uint16_t h[3];
         split3(w[i], h[0], h[1], h[2]);
 #pragma unroll
@@ -911,6 +986,10 @@ int rvz_resnet_fwd_f32(const float* x, int32_t n, const float* params, int32_t f
 }
 
 #ifdef RVZ_PHASE_TIMING
+int rvz_rt_read(uint64_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rt), (size_t)n * 2 * sizeof(uint64_t)) ==
+                   hipSuccess ? 0 : -5;
+}
 int rvz_wave_read(uint64_t* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave), (size_t)n * 16 * sizeof(uint64_t)) ==
                    hipSuccess ? 0 : -5;
@@ -953,13 +1032,12 @@ int rvz_resnet_trunk_split(const float* x, int32_t n, const float* params,
     const Layout L = make_layout(filters, blocks);
     hipStream_t s = (hipStream_t)stream;
     if (filters == 64) {
-        hipLaunchKernelGGL((k_resnet_split<64, 2, RVZ_SPLIT_TPW>), dim3((n + 1) / 2),
-                           dim3(512 / RVZ_SPLIT_TPW), 0, s, x, n, params, L, wsplit, blocks,
+        hipLaunchKernelGGL((k_resnet_split<SplitShape, 64, 2, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW>),
+                           dim3((n + 1) / 2), dim3(256), 0, s, x, n, params, L, wsplit, blocks,
                            work);
     } else if (filters == 128) {
-        hipLaunchKernelGGL((k_resnet_split<128, 1, RVZ_SPLIT_TPW>), dim3(n),
-                           dim3(512 / RVZ_SPLIT_TPW), 0, s, x, n, params, L, wsplit, blocks,
-                           work);
+        hipLaunchKernelGGL((k_resnet_split<SplitShape, 128, 1, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW>),
+                           dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
     } else {
         return RVZ_EINVAL;
     }

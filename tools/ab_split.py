@@ -40,9 +40,18 @@ ref_l, ref_v = ref_l.clone(), ref_v.clone()
 s = _lib.stream_handle()
 
 
-def run(lib):
+wsp = {}
+for name, lib in variants:   # each variant lays out its own split weights (MFMA shape)
+    lib.rvz_resnet_split_size.restype = C.c_int64
+    w = torch.empty(lib.rvz_resnet_split_size(filters, blocks), dtype=torch.int16, device="cuda")
+    assert lib.rvz_resnet_split_weights(C.c_void_p(ev.params.data_ptr()), filters, blocks,
+                                        C.c_void_p(w.data_ptr()), C.c_void_p(s)) == 0
+    wsp[name] = w
+
+
+def run(lib, name):
     rc = lib.rvz_resnet_fwd_split(C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
-                                  C.c_void_p(ev.wsplit.data_ptr()), filters, blocks,
+                                  C.c_void_p(wsp[name].data_ptr()), filters, blocks,
                                   C.c_void_p(wk.data_ptr()), C.c_void_p(lg.data_ptr()),
                                   C.c_void_p(v.data_ptr()), C.c_void_p(s))
     assert rc == 0
@@ -51,17 +60,17 @@ def run(lib):
 res = {name: [] for name, _ in variants}
 err = {}
 for name, lib in variants:
-    run(lib)
+    run(lib, name)
     torch.cuda.synchronize()
     err[name] = max((lg - ref_l).abs().max().item(), (v - ref_v).abs().max().item())
 for rep in range(5):
     for name, lib in variants:
         for _ in range(3):
-            run(lib)
+            run(lib, name)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for _ in range(20):
-            run(lib)
+            run(lib, name)
         b.record()
         torch.cuda.synchronize()
         res[name].append(a.elapsed_time(b) / 20)

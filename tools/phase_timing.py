@@ -62,5 +62,13 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
                 "l0_kloop": float((b[:, 4] - b[:, 1]).mean()),
                 "l0_epilogue": float((b[:, 5] - b[:, 4]).mean()),
                 "l0_barrier": float((b[:, 6] - b[:, 5]).mean()),
-                "span": int(buf[:, 3].max()) - int(buf[:, 0].min()), "n_wg": nwg}
+                "n_wg": nwg}
+    rt = np.zeros((nwg, 2), np.uint64)
+    assert lib.rvz_rt_read(rt.ctypes.data_as(C.c_void_p), nwg) == 0
+    rt = rt.astype(np.int64)
+    wg_us = (rt[:, 1] - rt[:, 0]) / 100.0                    # 100 MHz
+    out[key]["wg_us_mean"] = float(wg_us.mean())
+    out[key]["clock_ghz"] = float(tot.mean() / wg_us.mean() / 1e3)
+    out[key]["kernel_span_us"] = float((rt[:, 1].max() - rt[:, 0].min()) / 100.0)
+    out[key]["busy_frac"] = float(wg_us.sum() / 256 / out[key]["kernel_span_us"])
 print(json.dumps(out))
