@@ -599,9 +599,6 @@ struct CfgS {
 #ifndef RVZ_SPLIT_PD
 #define RVZ_SPLIT_PD 3       // weight prefetch distance, k-steps
 #endif
-#ifndef RVZ_STEM_MFMA
-#define RVZ_STEM_MFMA 1          // stem conv on the split MFMA (else VALU)
-#endif
 #ifndef RVZ_SPLIT_INTERLEAVE
 #define RVZ_SPLIT_INTERLEAVE 1   // loads placed between the MFMAs of a k-step
 #endif
@@ -627,15 +624,29 @@ struct WaveTiles {
 };
 
 // conv epilogue: bias (+ skip), ReLU, exact split back into the three parts; per register group
-// g of tile (c, u) the lane holds 4 consecutive channels of its pixel -> 8-byte reads/writes
-template <class S, int F, int NBOARD, int CTW, int PTW, bool RES>
+// g of tile (c, u) the lane holds 4 consecutive channels of its pixel -> 8-byte writes. The skip
+// input of a residual block is the block input, which this lane itself produced (same tile map
+// in the stem and every conv): it stays in registers (res, fp32 — the exact value its split
+// encodes), RES adds it, KEEP stores the result as the next block's skip input.
+template <class S, int CTW, int PTW, bool REGRES>
+struct EpiRegs {
+    f32x4 bias[CTW][S::NG];
+    float res[CTW][PTW][REGRES ? S::NG * 4 : 1];
+};
+// skip input in registers where they fit (F = 64); at F = 128 they would spill, and the epilogue
+// re-reads it from LDS (joining its split)
+template <int F>
+struct RegRes {
+    static constexpr bool value = F <= 64;
+};
+
+template <class S, int F, int NBOARD, int CTW, int PTW, bool RES, bool KEEP>
 __device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out,
                                                const typename S::acc_t (&hi)[CTW][PTW],
                                                const typename S::acc_t (&lo)[CTW][PTW],
-                                               const float* __restrict__ bias,
+                                               EpiRegs<S, CTW, PTW, RegRes<F>::value>& er,
                                                const WaveTiles<S, F, CTW, PTW>& wt, int lane) {
     using C = CfgS<S, F, NBOARD>;
-    typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
@@ -644,10 +655,11 @@ __device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out,
 #pragma unroll
             for (int g = 0; g < S::NG; ++g) {
                 const int n0 = (wt.ct0 + c) * S::TM + S::chan(g, lane);
-                const f32x4 bn = *reinterpret_cast<const f32x4*>(bias + n0);
                 uint16_t* o = out + wt.px[u] * C::CSB + n0;
+                constexpr bool REG = RegRes<F>::value;
+                typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
                 u16x4 s0, s1, s2;
-                if (RES) {
+                if (RES && !REG) {
                     s0 = *reinterpret_cast<const u16x4*>(o);
                     s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
                     s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
@@ -659,9 +671,13 @@ __device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out,
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         const int j = 2 * hf + e, reg = 4 * g + j;
-                        v[e] = (hi[c][u][reg] + lo[c][u][reg]) + bn[j];
-                        if (RES) v[e] += join3(s0[j], s1[j], s2[j]);   // skip input, in place
+                        v[e] = (hi[c][u][reg] + lo[c][u][reg]) + er.bias[c][g][j];
+                        if (RES) {                              // skip input
+                            if constexpr (REG) v[e] += er.res[c][u][reg];
+                            else v[e] += join3(s0[j], s1[j], s2[j]);
+                        }
                         v[e] = fmaxf(v[e], 0.0f);
+                        if constexpr (KEEP && REG) er.res[c][u][reg] = v[e];
                     }
                     uint32_t h0, h1, h2;
                     split3x2(v, h0, h1, h2);
@@ -673,6 +689,17 @@ __device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out,
                 *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
                 *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
             }
+}
+
+template <class S, int F, int CTW, int PTW>
+__device__ __forceinline__ void load_bias(EpiRegs<S, CTW, PTW, RegRes<F>::value>& er, const float* __restrict__ bias,
+                                          const WaveTiles<S, F, CTW, PTW>& wt, int lane) {
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int g = 0; g < S::NG; ++g)
+            er.bias[c][g] = *reinterpret_cast<const f32x4*>(bias + (wt.ct0 + c) * S::TM +
+                                                            S::chan(g, lane));
 }
 
 // 8 bf16 parts p of 8 fp32 values
@@ -702,8 +729,10 @@ __device__ constexpr int kTA[6] = {0, 2, 0, 1, 1, 0};
 template <class S, int F, int NBOARD, int CTW, int PTW>
 __device__ __forceinline__ void stem_split(const float* xin, uint16_t* __restrict__ out,
                                            const float* __restrict__ prm, const Layout& L,
-                                           int wave, int lane) {
+                                           int wave, int lane,
+                                           EpiRegs<S, CTW, PTW, RegRes<F>::value>& er) {
     const WaveTiles<S, F, CTW, PTW> wt(wave, lane);
+    load_bias(er, prm + L.stem_b, wt, lane);
     const int kq = 8 * (lane / S::TM);               // this lane's k offset in a step
     typename S::acc_t hi[CTW][PTW], lo[CTW][PTW];
 #pragma unroll
@@ -748,7 +777,7 @@ __device__ __forceinline__ void stem_split(const float* xin, uint16_t* __restric
                     acc = S::mfma(wq[c][kTW[term]], aq[u][kTA[term]], acc);
                 }
     }
-    epilogue_split<S, F, NBOARD, CTW, PTW, false>(out, hi, lo, prm + L.stem_b, wt, lane);
+    epilogue_split<S, F, NBOARD, CTW, PTW, false, true>(out, hi, lo, er, wt, lane);
 }
 
 // sched_group_barrier pattern: NM MFMAs, the first ND gaps get one LDS read, the next NV one
@@ -766,10 +795,13 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
                                            uint16_t* __restrict__ out,
                                            const uint16_t* __restrict__ wl,   // layer fragments
                                            const float* __restrict__ bias, int wave, int lane,
-                                           bf16x8 (&bc)[RVZ_SPLIT_PD][CTW][3], int ptag = -1) {
+                                           bf16x8 (&bc)[RVZ_SPLIT_PD][CTW][3],
+                                           EpiRegs<S, CTW, PTW, RegRes<F>::value>& er,
+                                           int ptag = -1) {
     using C = CfgS<S, F, NBOARD>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_SPLIT_PD;
     const WaveTiles<S, F, CTW, PTW> wt(wave, lane);
+    load_bias(er, bias, wt, lane);                  // lands during the k-loop
     const int kq = 8 * (lane / S::TM);
     // the taps of each of the lane's pixels that stay on its board
     unsigned pmask[PTW];
@@ -823,32 +855,34 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
                 }
     };
     // Software pipeline, fully unrolled (constant register indices, no copies of in-flight
-    // loads): step it computes while step it+2's activation fragments (LDS) and step it+PD's
+    // loads): step it computes while step it+APD's activation fragments (LDS) and step it+PD's
     // weight fragments (L2) load, one load per MFMA issue gap (an MFMA leaves most of its issue
     // cycles free; 9+ loads back to back would let the matrix pipe drain). bc carries the next
     // layer's first PD k-steps (layers are contiguous; the buffer has RVZ_SPLIT_PAD k-steps of
     // padding after the last).
+    // activation prefetch distance: 2 k-steps where the registers allow (F = 64), else 1
+    constexpr int APD = F <= 64 ? 2 : 1;
     bf16x8 bq[NIT + PD][CTW][3];
-    bf16x8 aq[3][PTW][3];
+    bf16x8 aq[APD + 1][PTW][3];
 #pragma unroll
     for (int d = 0; d < PD; ++d)
 #pragma unroll
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
             for (int p = 0; p < 3; ++p) bq[d][c][p] = bc[d][c][p];
-    load_a(aq[0], 0);
-    load_a(aq[1], 1);
+#pragma unroll
+    for (int d = 0; d < APD; ++d) load_a(aq[d], d);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-        if (it + 2 < NIT) load_a(aq[(it + 2) % 3], it + 2);
+        if (it + APD < NIT) load_a(aq[(it + APD) % (APD + 1)], it + APD);
         load_b(bq[it + PD], it + PD);
 #if RVZ_SPLIT_INTERLEAVE
-        compute(aq[it % 3], bq[it]);
+        compute(aq[it % (APD + 1)], bq[it]);
         interleave_loads<0, 6 * CTW * PTW, 3 * PTW, 3 * CTW>();
         __builtin_amdgcn_sched_barrier(0);
 #else
         __builtin_amdgcn_sched_barrier(0);
-        compute(aq[it % 3], bq[it]);
+        compute(aq[it % (APD + 1)], bq[it]);
         __builtin_amdgcn_sched_barrier(0);
 #endif
     }
@@ -862,7 +896,8 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
         PHASE(ptag);
         WAVE_T(0);
     }
-    epilogue_split<S, F, NBOARD, CTW, PTW, RES>(out, hi, lo, bias, wt, lane);
+    // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
+    epilogue_split<S, F, NBOARD, CTW, PTW, RES, RES>(out, hi, lo, er, wt, lane);
 }
 
 // one workgroup = 4 waves (one per SIMD) = NBOARD boards; wave tile CTW x PTW MFMA tiles
@@ -905,11 +940,8 @@ __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict
     load_input<NBOARD>(x, n_boards, g0, xin, tid, NTHR);
     __syncthreads();
     const ActSplit outA{actA, C::CSB, C::PLANE};
-#if RVZ_STEM_MFMA
-    stem_split<S, F, NBOARD, CTW, PTW>(xin, actA, prm, L, wave, lane);
-#else
-    stem<F, NBOARD, NTHR>(xin, outA, prm, L, tid);
-#endif
+    EpiRegs<S, CTW, PTW, RegRes<F>::value> er;      // bias and skip-input registers
+    stem_split<S, F, NBOARD, CTW, PTW>(xin, actA, prm, L, wave, lane, er);
     __syncthreads();
     PHASE(1);
     const int64_t LW = split_layer_elems(F);
@@ -917,7 +949,7 @@ __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict
         const int l1 = 2 * blk, l2 = 2 * blk + 1;
         conv_split<S, F, NBOARD, CTW, PTW, false>(actA, actB, wsp + l1 * LW,
                                                   prm + L.res_b + (size_t)l1 * F, wave, lane, bc,
-                                                  blk == 0 ? 4 : -1);
+                                                  er, blk == 0 ? 4 : -1);
         if (blk == 0) {
             PHASE(5);
             WAVE_T(1);
@@ -925,7 +957,8 @@ __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict
         __syncthreads();
         if (blk == 0) PHASE(6);
         conv_split<S, F, NBOARD, CTW, PTW, true>(actB, actA, wsp + l2 * LW,
-                                                 prm + L.res_b + (size_t)l2 * F, wave, lane, bc);
+                                                 prm + L.res_b + (size_t)l2 * F, wave, lane, bc,
+                                                 er);
         __syncthreads();
     }
     PHASE(2);

@@ -22,9 +22,14 @@ variants = []
 for item in os.environ.get("RVZ_AB", "base:").split(";"):
     name, flags = item.split(":", 1)
     so = f"/tmp/librvz_ab_{name}.so"
+    path = src
+    if flags.startswith("@"):          # "@<source file> <flags>": another revision of the source
+        path, _, flags = flags[1:].partition(" ")
+        path = os.path.join(ROOT, path)
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                            "-fPIC", "-ffp-contract=off", "-fno-gpu-flush-denormals-to-zero",
-                           *flags.split(), "-shared", "-o", so, src])
+                           "-I", os.path.dirname(src), "-x", "hip", *flags.split(), "-shared",
+                           "-o", so, path])
     variants.append((name, C.CDLL(so)))
 
 blocks, filters, n = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (6, 64, 4096)))
