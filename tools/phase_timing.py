@@ -63,6 +63,15 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
                 "l0_epilogue": float((b[:, 5] - b[:, 4]).mean()),
                 "l0_barrier": float((b[:, 6] - b[:, 5]).mean()),
                 "n_wg": nwg}
+    if hasattr(lib, "rvz_stem_read"):    # builds with the stem stamps (STEM_T)
+        st = np.zeros((nwg, 4), np.uint64)
+        assert lib.rvz_stem_read(st.ctypes.data_as(C.c_void_p), nwg) == 0
+        st = st.astype(np.int64)
+        out[key]["stem_split"] = {"loads_zero": float((st[:, 0] - b[:, 0]).mean()),
+                                  "sync1": float((st[:, 1] - st[:, 0]).mean()),
+                                  "xin_write_sync2": float((st[:, 2] - st[:, 1]).mean()),
+                                  "stem_compute": float((st[:, 3] - st[:, 2]).mean()),
+                                  "sync3": float((b[:, 1] - st[:, 3]).mean())}
     rt = np.zeros((nwg, 2), np.uint64)
     assert lib.rvz_rt_read(rt.ctypes.data_as(C.c_void_p), nwg) == 0
     rt = rt.astype(np.int64)
