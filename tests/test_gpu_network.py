@@ -126,3 +126,25 @@ def test_split_error_is_fp32_class(blocks, filters, n):
     fp32 = max(err["resnet"], err["module"])
     assert err["split"] <= 4 * fp32 + 1e-7 * scale, (err, scale)
     assert err["split"] <= 1e-5 * scale, (err, scale)
+
+
+@pytest.mark.parametrize("kernel", ["split", "resnet", "miopen"])
+def test_evaluator_matches_reference_outputs(kernel):
+    """Every NN call of the reference's S=800 6x64 self-play fixture (1,499 leaf positions):
+    the GPU evaluator's softmax rows and values against the reference's own recorded outputs
+    (CPU fp32 PyTorch). The net is the fixture's (seed 0, pinned bit-exactly on CPU by
+    test_network_cpu.py). Tolerance: fp32 evaluation-order differences."""
+    import os
+    import rvz
+    from test_network_cpu import fixture_planes
+    x, probs, value = fixture_planes(os.path.join(os.path.dirname(__file__), "golden",
+                                                  "mcts_s800_6x64.npz"))
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
+    ev = rvz.LeafEvaluator(net, kernel=kernel)
+    logits, v = ev(torch.from_numpy(x).cuda())
+    p = torch.softmax(logits, 1).cpu().numpy()
+    dp = np.abs(p - probs).max()
+    dv = np.abs(v.cpu().numpy() - value).max()
+    assert dp <= 1e-5 and dv <= 1e-5, (dp, dv)
+    assert (p.argmax(1) == probs.argmax(1)).mean() > 0.99

@@ -40,3 +40,34 @@ def test_leaf_evaluator_folded_bn_cpu():
     np.testing.assert_allclose(logits.numpy(), d["logits"], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(value.numpy(), d["value"], rtol=1e-4, atol=1e-5)
     assert ev.flops_per_row() > 0
+
+
+def fixture_planes(path, n=None):
+    """The recorded leaf positions of a reference self-play fixture as [n,3,8,8] planes
+    (call_masks: three bitmasks per call, square s = bit s), with the reference's own softmax
+    rows and values for them (make_golden.py _Recorder: mcts.py:596-597)."""
+    with np.load(path) as z:
+        m, probs, value = z["call_masks"], z["call_probs"], z["call_value"]
+    if n is not None:
+        m, probs, value = m[:n], probs[:n], value[:n]
+    x = np.zeros((len(m), 3, 8, 8), np.float32)
+    for i in range(3):
+        bits = (m[:, i:i + 1] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)
+        x[:, i] = bits.astype(np.float32).reshape(-1, 8, 8)
+    return x, probs, value
+
+
+def test_seeded_6x64_net_reproduces_reference_fixture():
+    """torch.manual_seed(0) + rvz.AlphaZeroNetwork(8, 6, 64) is the reference's 6x64 net of the
+    S=800 fixture (same module order and init): on CPU it reproduces the reference's recorded
+    softmax rows and values bit for bit, which pins the GPU evaluators against the reference's
+    own outputs (tests/test_gpu_network.py)."""
+    import rvz
+    x, probs, value = fixture_planes(os.path.join(os.path.dirname(__file__), "golden",
+                                                  "mcts_s800_6x64.npz"), n=256)
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 6, 64).eval()
+    with torch.no_grad():
+        logits, v = net(torch.from_numpy(x))
+    assert np.array_equal(torch.softmax(logits, 1).numpy(), probs)
+    assert np.array_equal(v.numpy().reshape(-1), value)
