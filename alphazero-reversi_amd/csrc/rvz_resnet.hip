@@ -54,8 +54,9 @@ struct Layout {
 
 __host__ __device__ inline int64_t al4(int64_t o) { return (o + 3) & ~int64_t(3); }
 
-__host__ __device__ inline Layout make_layout(int F, int NB) {
+__host__ __device__ inline Layout make_layout(int F, int NB, int BS = 8) {
     Layout L;
+    const int cells = BS * BS;
     int64_t o = 0;
     L.stem_w = o; o = al4(o + (int64_t)F * 27);
     L.stem_b = o; o = al4(o + F);
@@ -63,11 +64,11 @@ __host__ __device__ inline Layout make_layout(int F, int NB) {
     L.res_b = o;  o = al4(o + (int64_t)2 * NB * F);
     L.pol_w = o;  o = al4(o + 2 * F);
     L.pol_b = o;  o = al4(o + 2);
-    L.pfc_w = o;  o = al4(o + 65 * 128);
-    L.pfc_b = o;  o = al4(o + 65);
+    L.pfc_w = o;  o = al4(o + (int64_t)(cells + 1) * 2 * cells);
+    L.pfc_b = o;  o = al4(o + cells + 1);
     L.val_w = o;  o = al4(o + F);
     L.val_b = o;  o = al4(o + 1);
-    L.vfc1_w = o; o = al4(o + 256 * 64);
+    L.vfc1_w = o; o = al4(o + 256 * cells);
     L.vfc1_b = o; o = al4(o + 256);
     L.vfc2_w = o; o = al4(o + 256);
     L.vfc2_b = o; o = al4(o + 1);
@@ -158,17 +159,20 @@ struct ActSplit {
     }
 };
 
-// leaf planes x[g][3][8][8] -> xin[b][10x10 padded pixel][4] (halo 0)
-template <int NBOARD>
+// leaf planes x[g][3][BS][BS] -> xin[b][10x10 padded pixel][4] (halo and, for BS < 8, the
+// unused rows/columns 0)
+template <int NBOARD, int BS = 8>
 __device__ __forceinline__ void load_input(const float* __restrict__ x, int n_boards, int g0,
                                            float* xin, int tid, int nthr) {
+    constexpr int CELLS = BS * BS;
     for (int i = tid; i < NBOARD * 100 * 4; i += nthr) xin[i] = 0.0f;
     __syncthreads();
-    for (int i = tid; i < NBOARD * 192; i += nthr) {
-        const int b = i / 192, rem = i % 192, ch = rem / 64, px = rem % 64;
+    for (int i = tid; i < NBOARD * 3 * CELLS; i += nthr) {
+        const int b = i / (3 * CELLS), rem = i % (3 * CELLS), ch = rem / CELLS,
+                  cell = rem % CELLS;
         const int g = g0 + b;
-        const float v = g < n_boards ? x[(size_t)g * 192 + rem] : 0.0f;
-        xin[(b * 100 + (px / 8 + 1) * 10 + (px % 8) + 1) * 4 + ch] = v;
+        const float v = g < n_boards ? x[(size_t)g * 3 * CELLS + rem] : 0.0f;
+        xin[(b * 100 + (cell / BS + 1) * 10 + (cell % BS) + 1) * 4 + ch] = v;
     }
 }
 
@@ -201,10 +205,11 @@ __device__ __forceinline__ void stem(const float* xin, const Act& act, const flo
 
 // heads (network.py:104-117), part 1: the 1x1 convs (BN folded) + ReLU of both heads, in one
 // pass over the activations: lane = pixel, wave = (board, channel group), partial sums per group
-// through LDS (`part`, the free ping-pong buffer) added in a fixed order. Writes, per board b,
-// hpv(b)[0..127] = the policy planes (NCHW flatten, the FC's input order) and hpv(b)[128..191] =
-// the value plane.
-template <int F, int NBOARD, int NTHR, class Act, class Out>
+// through LDS (`part`, the free ping-pong buffer) added in a fixed order. Writes, per board b
+// (cells = BS*BS), hpv(b)[0 .. 2 cells) = the policy planes (NCHW flatten, the FC's input order)
+// and hpv(b)[2 cells .. 3 cells) = the value plane. A BS < 8 board sits in the top-left corner
+// of the 8x8 pixel grid.
+template <int F, int NBOARD, int NTHR, int BS = 8, class Act, class Out>
 __device__ __forceinline__ void head_convs(const Act& act, float* part,
                                            const float* __restrict__ prm, const Layout& L,
                                            const Out& hpv, int tid) {
@@ -234,14 +239,16 @@ __device__ __forceinline__ void head_convs(const Act& act, float* part,
         part[(cg * 3 + 2) * NBOARD * 64 + row] = p2;
     }
     __syncthreads();
-    for (int o = tid; o < NBOARD * 192; o += NTHR) {
-        const int c2 = o / (NBOARD * 64), row = o % (NBOARD * 64);   // row = b*64 + px
+    constexpr int CELLS = BS * BS;
+    for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
+        const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
+        const int b = rem / CELLS, cell = rem % CELLS;
+        const int row = b * 64 + (cell / BS) * 8 + cell % BS;      // pixel of the 8x8 grid
         float acc = 0.0f;
 #pragma unroll
         for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * NBOARD * 64 + row];
-        const int b = row >> 6, px = row & 63;
         const float bias = c2 < 2 ? prm[L.pol_b + c2] : prm[L.val_b];
-        hpv.store(b, c2 * 64 + px, fmaxf(acc + bias, 0.0f));
+        hpv.store(b, c2 * CELLS + cell, fmaxf(acc + bias, 0.0f));
     }
 }
 
@@ -314,34 +321,41 @@ __device__ __forceinline__ void head_fcs(const float* hpv, float* h1,
 // heads, part 2 as its own launch over FCB boards per workgroup (the split path): each FC weight
 // row is loaded once per workgroup into registers and applied to all FCB boards (LDS broadcast
 // inputs) — inside the trunk kernel the same weights streamed from L2 once per 2 boards, with
-// the matrix cores idle. Thread t: value-fc1 row t; threads < 130: half of policy row t/2.
+// the matrix cores idle. Thread t: value-fc1 row t; threads < 2*(cells+1): half of policy row
+// t/2. work rows: [2 cells policy planes | cells value plane], stride 192.
 #ifndef RVZ_FCB
 #define RVZ_FCB 8
 #endif
 constexpr int FCB = RVZ_FCB;   // boards per workgroup (multiple of 4)
+template <int BS>
 __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work, int n,
                                                   const float* __restrict__ prm, Layout L,
                                                   float* __restrict__ logits,
                                                   float* __restrict__ value) {
-    __shared__ __attribute__((aligned(16))) float in[FCB][192];
+    constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1, ROW = 3 * CELLS;
+    constexpr int VQ = CELLS / 4, PQ = PIN / 2 / 4;   // f32x4 per value row / policy half-row
+    static_assert(CELLS % 4 == 0 && 2 * POUT <= 256, "thread map");
+    __shared__ __attribute__((aligned(16))) float in[FCB][ROW];
     __shared__ __attribute__((aligned(16))) float h1[FCB][256];
-    __shared__ float pp[FCB][130];
+    __shared__ float pp[FCB][2 * POUT];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g0 = blockIdx.x * FCB, nb = n - g0 < FCB ? n - g0 : FCB;
-    f32x4 wv[16], wp[16];
+    f32x4 wv[VQ], wp[PQ];
     {
-        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + tid * 64);
+        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + tid * CELLS);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) wv[i] = r[i];
+        for (int i = 0; i < VQ; ++i) wv[i] = r[i];
     }
-    if (tid < 130) {
-        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.pfc_w + (tid >> 1) * 128 +
-                                                         (tid & 1) * 64);
+    if (tid < 2 * POUT) {
+        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.pfc_w + (tid >> 1) * PIN +
+                                                         (tid & 1) * (PIN / 2));
 #pragma unroll
-        for (int i = 0; i < 16; ++i) wp[i] = r[i];
+        for (int i = 0; i < PQ; ++i) wp[i] = r[i];
     }
-    for (int i = tid; i < FCB * 192; i += 256)
-        (&in[0][0])[i] = i < nb * 192 ? work[(size_t)g0 * 192 + i] : 0.0f;
+    for (int i = tid; i < FCB * ROW; i += 256) {
+        const int b = i / ROW, k = i % ROW;
+        (&in[0][0])[i] = b < nb ? work[(size_t)(g0 + b) * 192 + k] : 0.0f;
+    }
     __syncthreads();
     // 4 boards at a time: four independent FMA chains per thread
     constexpr int IL = 4;
@@ -351,10 +365,10 @@ __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work
 #pragma unroll
         for (int j = 0; j < IL; ++j) acc[j] = b1;
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
+        for (int i = 0; i < VQ; ++i)
 #pragma unroll
             for (int j = 0; j < IL; ++j) {
-                const f32x4 x = reinterpret_cast<const f32x4*>(&in[b0 + j][128])[i];
+                const f32x4 x = reinterpret_cast<const f32x4*>(&in[b0 + j][PIN])[i];
                 acc[j] = fmaf(x[0], wv[i][0], acc[j]);
                 acc[j] = fmaf(x[1], wv[i][1], acc[j]);
                 acc[j] = fmaf(x[2], wv[i][2], acc[j]);
@@ -363,14 +377,15 @@ __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work
 #pragma unroll
         for (int j = 0; j < IL; ++j) h1[b0 + j][tid] = fmaxf(acc[j], 0.0f);
     }
-    if (tid < 130) {
+    if (tid < 2 * POUT) {
         for (int b0 = 0; b0 < FCB; b0 += IL) {
             float acc[IL] = {};
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
+            for (int i = 0; i < PQ; ++i)
 #pragma unroll
                 for (int j = 0; j < IL; ++j) {
-                    const f32x4 x = reinterpret_cast<const f32x4*>(&in[b0 + j][(tid & 1) * 64])[i];
+                    const f32x4 x =
+                        reinterpret_cast<const f32x4*>(&in[b0 + j][(tid & 1) * (PIN / 2)])[i];
                     acc[j] = fmaf(x[0], wp[i][0], acc[j]);
                     acc[j] = fmaf(x[1], wp[i][1], acc[j]);
                     acc[j] = fmaf(x[2], wp[i][2], acc[j]);
@@ -381,9 +396,10 @@ __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work
         }
     }
     __syncthreads();
-    for (int o = tid; o < nb * 65; o += 256) {
-        const int b = o / 65, r = o % 65;
-        logits[(size_t)(g0 + b) * 65 + r] = prm[L.pfc_b + r] + (pp[b][2 * r] + pp[b][2 * r + 1]);
+    for (int o = tid; o < nb * POUT; o += 256) {
+        const int b = o / POUT, r = o % POUT;
+        logits[(size_t)(g0 + b) * POUT + r] =
+            prm[L.pfc_b + r] + (pp[b][2 * r] + pp[b][2 * r + 1]);
     }
     for (int b = wave; b < nb; b += 4) {
         float acc = 0.0f;
@@ -790,7 +806,7 @@ __device__ __forceinline__ void interleave_loads() {
     if constexpr (I + 1 < NM) interleave_loads<I + 1, NM, ND, NV>();
 }
 
-template <class S, int F, int NBOARD, int CTW, int PTW, bool RES>
+template <class S, int F, int NBOARD, int CTW, int PTW, bool RES, int BS = 8>
 __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
                                            uint16_t* __restrict__ out,
                                            const uint16_t* __restrict__ wl,   // layer fragments
@@ -811,7 +827,8 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
         unsigned msk = 0;
 #pragma unroll
         for (int t = 0; t < 9; ++t)
-            if ((unsigned)(rr + t / 3 - 1) < 8u && (unsigned)(cc + t % 3 - 1) < 8u) msk |= 1u << t;
+            if ((unsigned)(rr + t / 3 - 1) < (unsigned)BS && (unsigned)(cc + t % 3 - 1) < (unsigned)BS)
+                msk |= 1u << t;
         pmask[u] = msk;
     }
     typename S::acc_t hi[CTW][PTW], lo[CTW][PTW];
@@ -901,7 +918,7 @@ __device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
 }
 
 // one workgroup = 4 waves (one per SIMD) = NBOARD boards; wave tile CTW x PTW MFMA tiles
-template <class S, int F, int NBOARD, int CTW, int PTW>
+template <class S, int F, int NBOARD, int CTW, int PTW, int BS>
 __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict__ x,
                                                          int n_boards,
                                                          const float* __restrict__ prm, Layout L,
@@ -937,7 +954,7 @@ __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict
 #pragma unroll
                 for (int p = 0; p < 3; ++p) bc[s][c][p] = wf[((s * 3 + p) * C::CT + c) * 64];
     }
-    load_input<NBOARD>(x, n_boards, g0, xin, tid, NTHR);
+    load_input<NBOARD, BS>(x, n_boards, g0, xin, tid, NTHR);
     __syncthreads();
     const ActSplit outA{actA, C::CSB, C::PLANE};
     EpiRegs<S, CTW, PTW, RegRes<F>::value> er;      // bias and skip-input registers
@@ -947,7 +964,7 @@ __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict
     const int64_t LW = split_layer_elems(F);
     for (int blk = 0; blk < n_blocks; ++blk) {
         const int l1 = 2 * blk, l2 = 2 * blk + 1;
-        conv_split<S, F, NBOARD, CTW, PTW, false>(actA, actB, wsp + l1 * LW,
+        conv_split<S, F, NBOARD, CTW, PTW, false, BS>(actA, actB, wsp + l1 * LW,
                                                   prm + L.res_b + (size_t)l1 * F, wave, lane, bc,
                                                   er, blk == 0 ? 4 : -1);
         if (blk == 0) {
@@ -956,14 +973,14 @@ __global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict
         }
         __syncthreads();
         if (blk == 0) PHASE(6);
-        conv_split<S, F, NBOARD, CTW, PTW, true>(actB, actA, wsp + l2 * LW,
+        conv_split<S, F, NBOARD, CTW, PTW, true, BS>(actB, actA, wsp + l2 * LW,
                                                  prm + L.res_b + (size_t)l2 * F, wave, lane, bc,
                                                  er);
         __syncthreads();
     }
     PHASE(2);
-    head_convs<F, NBOARD, NTHR>(outA, reinterpret_cast<float*>(actB), prm, L,
-                                HeadsGlobal{work, g0, n_boards}, tid);
+    head_convs<F, NBOARD, NTHR, BS>(outA, reinterpret_cast<float*>(actB), prm, L,
+                                    HeadsGlobal{work, g0, n_boards}, tid);
     PHASE(3);
     RT(1);
 }
@@ -990,16 +1007,34 @@ __global__ void k_split_weights(const float* __restrict__ w, int F, int64_t tota
 
 }  // namespace
 
-extern "C" {
-
-int64_t rvz_resnet_params_size(int32_t filters, int32_t blocks) {
-    if ((filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
-    return make_layout(filters, blocks).total;
+template <int BS>
+static void launch_trunk(const float* x, int32_t n, const float* params, const uint16_t* wsplit,
+                         int32_t filters, int32_t blocks, float* work, hipStream_t s) {
+    const Layout L = make_layout(filters, blocks, BS);
+    if (filters == 64)
+        hipLaunchKernelGGL((k_resnet_split<SplitShape, 64, 2, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW, BS>),
+                           dim3((n + 1) / 2), dim3(256), 0, s, x, n, params, L, wsplit, blocks,
+                           work);
+    else
+        hipLaunchKernelGGL((k_resnet_split<SplitShape, 128, 1, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW, BS>),
+                           dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
 }
 
-int rvz_resnet_fwd_f32(const float* x, int32_t n, const float* params, int32_t filters,
-                       int32_t blocks, float* logits, float* value, void* stream) {
-    if (!x || !params || !logits || !value || n < 0 || blocks < 0) return RVZ_EINVAL;
+
+extern "C" {
+
+static bool board_ok(int32_t bs) { return bs == 8 || bs == 6; }
+
+int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks) {
+    if ((filters != 64 && filters != 128) || blocks < 0 || !board_ok(board)) return RVZ_EINVAL;
+    return make_layout(filters, blocks, board).total;
+}
+
+int rvz_resnet_fwd_f32(int32_t board, const float* x, int32_t n, const float* params,
+                       int32_t filters, int32_t blocks, float* logits, float* value,
+                       void* stream) {
+    if (board != 8 || !x || !params || !logits || !value || n < 0 || blocks < 0)
+        return RVZ_EINVAL;
     if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     const Layout L = make_layout(filters, blocks);
@@ -1055,48 +1090,47 @@ int rvz_resnet_split_weights(const float* params, int32_t filters, int32_t block
 
 int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192; }
 
-int rvz_resnet_trunk_split(const float* x, int32_t n, const float* params,
+int rvz_resnet_trunk_split(int32_t board, const float* x, int32_t n, const float* params,
                            const uint16_t* wsplit, int32_t filters, int32_t blocks, float* work,
                            void* stream) {
-    if (!x || !params || (!wsplit && blocks > 0) || !work || n < 0 || blocks < 0)
+    if (!x || !params || (!wsplit && blocks > 0) || !work || n < 0 || blocks < 0 ||
+        !board_ok(board) || (filters != 64 && filters != 128))
         return RVZ_EINVAL;
     if (((uintptr_t)params & 15) != 0 || ((uintptr_t)wsplit & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
-    const Layout L = make_layout(filters, blocks);
     hipStream_t s = (hipStream_t)stream;
-    if (filters == 64) {
-        hipLaunchKernelGGL((k_resnet_split<SplitShape, 64, 2, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW>),
-                           dim3((n + 1) / 2), dim3(256), 0, s, x, n, params, L, wsplit, blocks,
-                           work);
-    } else if (filters == 128) {
-        hipLaunchKernelGGL((k_resnet_split<SplitShape, 128, 1, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW>),
-                           dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
-    } else {
-        return RVZ_EINVAL;
-    }
+    if (board == 8) launch_trunk<8>(x, n, params, wsplit, filters, blocks, work, s);
+    else launch_trunk<6>(x, n, params, wsplit, filters, blocks, work, s);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
-int rvz_resnet_heads_fc(const float* work, int32_t n, const float* params, int32_t filters,
-                        int32_t blocks, float* logits, float* value, void* stream) {
-    if (!work || !params || !logits || !value || n < 0 || blocks < 0 ||
+int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float* params,
+                        int32_t filters, int32_t blocks, float* logits, float* value,
+                        void* stream) {
+    if (!work || !params || !logits || !value || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128))
         return RVZ_EINVAL;
     if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
-    const Layout L = make_layout(filters, blocks);
-    hipLaunchKernelGGL(k_heads_fc, dim3((n + FCB - 1) / FCB), dim3(256), 0, (hipStream_t)stream,
-                       work, n, params, L, logits, value);
+    const Layout L = make_layout(filters, blocks, board);
+    const dim3 grid((n + FCB - 1) / FCB), block(256);
+    if (board == 8)
+        hipLaunchKernelGGL(k_heads_fc<8>, grid, block, 0, (hipStream_t)stream, work, n, params,
+                           L, logits, value);
+    else
+        hipLaunchKernelGGL(k_heads_fc<6>, grid, block, 0, (hipStream_t)stream, work, n, params,
+                           L, logits, value);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
-int rvz_resnet_fwd_split(const float* x, int32_t n, const float* params, const uint16_t* wsplit,
-                         int32_t filters, int32_t blocks, float* work, float* logits,
-                         float* value, void* stream) {
+int rvz_resnet_fwd_split(int32_t board, const float* x, int32_t n, const float* params,
+                         const uint16_t* wsplit, int32_t filters, int32_t blocks, float* work,
+                         float* logits, float* value, void* stream) {
     if (!logits || !value) return RVZ_EINVAL;
-    const int rc = rvz_resnet_trunk_split(x, n, params, wsplit, filters, blocks, work, stream);
+    const int rc =
+        rvz_resnet_trunk_split(board, x, n, params, wsplit, filters, blocks, work, stream);
     if (rc != RVZ_OK) return rc;
-    return rvz_resnet_heads_fc(work, n, params, filters, blocks, logits, value, stream);
+    return rvz_resnet_heads_fc(board, work, n, params, filters, blocks, logits, value, stream);
 }
 
 }  // extern "C"

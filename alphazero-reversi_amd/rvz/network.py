@@ -156,14 +156,18 @@ class LeafEvaluator:
         #   "resnet" = the f32-input MFMA (rvz_resnet_fwd_f32);
         # "miopen" = PyTorch convs (+ the fused epilogue); "auto" = split where it applies
         self.n_blocks, self.filters = len(net.res_blocks), net.num_filters
-        resnet_ok = (dev.type == "cuda" and dtype == torch.float32 and net.board_size == 8
-                     and net.num_filters in (64, 128))
+        self.board_size = net.board_size
+        split_ok = (dev.type == "cuda" and dtype == torch.float32 and net.board_size in (6, 8)
+                    and net.num_filters in (64, 128))
         if kernel not in ("auto", "split", "resnet", "miopen"):
             raise ValueError(f"unknown kernel {kernel!r}")
-        if kernel in ("split", "resnet") and not resnet_ok:
-            raise ValueError("the fused resnet kernels need fp32, 8x8, 64 or 128 filters, a GPU")
+        if kernel == "split" and not split_ok:
+            raise ValueError("the split resnet kernel needs fp32, 8x8 or 6x6, 64 or 128 filters, "
+                             "a GPU")
+        if kernel == "resnet" and not (split_ok and net.board_size == 8):
+            raise ValueError("the f32 resnet kernel needs fp32, 8x8, 64 or 128 filters, a GPU")
         if kernel == "auto":
-            kernel = "split" if resnet_ok else "miopen"
+            kernel = "split" if split_ok else "miopen"
         self.kernel = kernel
         self.use_resnet = kernel in ("split", "resnet")
         self._outs = {}
@@ -172,7 +176,7 @@ class LeafEvaluator:
             lib = _lib.load()
             with torch.no_grad():
                 self.params = pack_resnet_params(net).to(dev).contiguous()
-            want = lib.rvz_resnet_params_size(self.filters, self.n_blocks)
+            want = lib.rvz_resnet_params_size(self.board_size, self.filters, self.n_blocks)
             if want != self.params.numel():
                 raise _lib.RvzError(f"packed params {self.params.numel()} != layout {want}")
             self.wsplit = None
@@ -243,14 +247,14 @@ class LeafEvaluator:
         logits, value, work = outs
         if self.wsplit is not None:
             _lib.check(_lib.load().rvz_resnet_fwd_split(
-                x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(), self.filters,
-                self.n_blocks, work.data_ptr(), logits.data_ptr(), value.data_ptr(),
-                _lib.stream_handle(x.device)), None, "rvz_resnet_fwd_split")
+                self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
+                self.filters, self.n_blocks, work.data_ptr(), logits.data_ptr(),
+                value.data_ptr(), _lib.stream_handle(x.device)), None, "rvz_resnet_fwd_split")
         else:
             _lib.check(_lib.load().rvz_resnet_fwd_f32(
-                x.data_ptr(), n, self.params.data_ptr(), self.filters, self.n_blocks,
-                logits.data_ptr(), value.data_ptr(), _lib.stream_handle(x.device)),
-                None, "rvz_resnet_fwd_f32")
+                self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.filters,
+                self.n_blocks, logits.data_ptr(), value.data_ptr(),
+                _lib.stream_handle(x.device)), None, "rvz_resnet_fwd_f32")
         return logits, value
 
     def trunk_only(self, x: torch.Tensor):
@@ -263,14 +267,15 @@ class LeafEvaluator:
             self(x)                                # allocates the per-batch buffers
         work = self._outs[x.shape[0]][2]
         _lib.check(_lib.load().rvz_resnet_trunk_split(
-            x.data_ptr(), x.shape[0], self.params.data_ptr(), self.wsplit.data_ptr(),
-            self.filters, self.n_blocks, work.data_ptr(), _lib.stream_handle(x.device)),
-            None, "rvz_resnet_trunk_split")
+            self.board_size, x.data_ptr(), x.shape[0], self.params.data_ptr(),
+            self.wsplit.data_ptr(), self.filters, self.n_blocks, work.data_ptr(),
+            _lib.stream_handle(x.device)), None, "rvz_resnet_trunk_split")
 
     def mfma_flops_per_row(self) -> int:
         """FLOPs the split trunk kernel executes on the bf16 matrix cores per board: six partial
-        products per fp32 product, stem K padded 27 -> 32."""
-        cells, f = self.board_size ** 2, self.filters
+        products per fp32 product, stem K padded 27 -> 32, over the 8x8 pixel grid (a 6x6 board
+        is computed embedded in it)."""
+        cells, f = 64, self.filters
         return 6 * 2 * cells * f * (32 + 2 * self.n_blocks * 9 * f)
 
     @torch.no_grad()

@@ -140,35 +140,38 @@ int rvz_nn_bias_act_bf16(void *x, const float *bias, const void *residual, int64
                          int32_t channels, int32_t relu, void *hip_stream);
 
 /* The whole policy/value network forward (network.py:30-117, BN folded) in one kernel: x float32
- * [n, 3, 8, 8] (the leaf planes) -> logits float32 [n, 65], value float32 [n]. fp32 on the
- * f32-input MFMA, activations resident in LDS. filters 64 (2 boards per workgroup) or 128
- * (1 board per workgroup), any block count. params: the packed fp32 buffer laid out as in
- * csrc/rvz_resnet.hip (rvz.network.pack_resnet_params), 16-byte aligned, of
- * rvz_resnet_params_size(filters, blocks) floats (negative: unsupported shape). */
-int64_t rvz_resnet_params_size(int32_t filters, int32_t blocks);
-int rvz_resnet_fwd_f32(const float *x, int32_t n, const float *params, int32_t filters,
-                       int32_t blocks, float *logits, float *value, void *hip_stream);
+ * [n, 3, board, board] (the leaf planes) -> logits float32 [n, board^2 + 1], value float32 [n].
+ * params: the packed fp32 buffer laid out as in csrc/rvz_resnet.hip
+ * (rvz.network.pack_resnet_params), 16-byte aligned, of rvz_resnet_params_size(board, filters,
+ * blocks) floats (negative: unsupported shape). filters 64 or 128, any block count.
+ * rvz_resnet_fwd_f32: board 8 only; fp32 on the f32-input MFMA, activations resident in LDS. */
+int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks);
+int rvz_resnet_fwd_f32(int32_t board, const float *x, int32_t n, const float *params,
+                       int32_t filters, int32_t blocks, float *logits, float *value,
+                       void *hip_stream);
 
 /* The same forward with fp32 arithmetic emulated on the bf16 MFMA: every operand split exactly
  * into three bf16 parts (x = x0 + (x1 + x2)) and the six partial products of weight >= 2^-16
- * accumulated in fp32 (error of an fp32 GEMM; see csrc/rvz_resnet.hip). wsplit: the conv weights
- * re-laid out by rvz_resnet_split_weights from the packed params (once per parameter update),
- * rvz_resnet_split_size(filters, blocks) uint16 elements, 16-byte aligned. work: float scratch of
- * rvz_resnet_work_size(n) elements (the 1x1-conv head outputs handed to the FC launch). */
+ * accumulated in fp32 (error of an fp32 GEMM; see csrc/rvz_resnet.hip). Boards 8 and 6.
+ * wsplit: the conv weights re-laid out by rvz_resnet_split_weights from the packed params (once
+ * per parameter update), rvz_resnet_split_size(filters, blocks) uint16 elements, 16-byte
+ * aligned. work: float scratch of rvz_resnet_work_size(n) elements (the 1x1-conv head outputs
+ * handed to the FC launch). */
 int64_t rvz_resnet_split_size(int32_t filters, int32_t blocks);
 int rvz_resnet_split_weights(const float *params, int32_t filters, int32_t blocks,
                              uint16_t *wsplit, void *hip_stream);
 int64_t rvz_resnet_work_size(int32_t n);
-int rvz_resnet_fwd_split(const float *x, int32_t n, const float *params, const uint16_t *wsplit,
-                         int32_t filters, int32_t blocks, float *work, float *logits,
-                         float *value, void *hip_stream);
+int rvz_resnet_fwd_split(int32_t board, const float *x, int32_t n, const float *params,
+                         const uint16_t *wsplit, int32_t filters, int32_t blocks, float *work,
+                         float *logits, float *value, void *hip_stream);
 /* rvz_resnet_fwd_split's two launches on their own: the trunk (stem, residual tower, 1x1 head
  * convs -> work) and the batched FC heads (work -> logits, value). */
-int rvz_resnet_trunk_split(const float *x, int32_t n, const float *params,
+int rvz_resnet_trunk_split(int32_t board, const float *x, int32_t n, const float *params,
                            const uint16_t *wsplit, int32_t filters, int32_t blocks, float *work,
                            void *hip_stream);
-int rvz_resnet_heads_fc(const float *work, int32_t n, const float *params, int32_t filters,
-                        int32_t blocks, float *logits, float *value, void *hip_stream);
+int rvz_resnet_heads_fc(int32_t board, const float *work, int32_t n, const float *params,
+                        int32_t filters, int32_t blocks, float *logits, float *value,
+                        void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -86,6 +86,31 @@ def _bn_net(blocks, filters, seed=3):
     return net
 
 
+@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 1000), (2, 128, 33), (0, 64, 1)])
+def test_split_kernel_6x6_matches_module(blocks, filters, n):
+    """The split kernel on the 6x6 variant (config 5): the board sits in the top-left corner of
+    the 8x8 pixel grid, taps past row/column 5 read zero, the heads see the 36 cells."""
+    import rvz
+    torch.manual_seed(4)
+    net = rvz.AlphaZeroNetwork(6, blocks, filters).cuda().eval()
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    x = (torch.rand(n, 3, 6, 6, device="cuda") > 0.6).float()
+    with torch.no_grad():
+        lr, vr = net(x)
+    ev = rvz.LeafEvaluator(net)
+    assert ev.kernel == "split"
+    l, v = ev(x)
+    torch.cuda.synchronize()
+    assert l.shape == (n, 37)
+    scale = lr.abs().max().item()
+    assert (l - lr).abs().max().item() <= 2e-5 * scale
+    assert (v - vr).abs().max().item() <= 2e-3
+
+
 @pytest.mark.parametrize("kernel", ["resnet", "split"])
 @pytest.mark.parametrize("blocks,filters,n", [(6, 64, 4096), (10, 128, 515), (1, 64, 3), (0, 128, 2)])
 def test_resnet_kernel_matches_module(kernel, blocks, filters, n):

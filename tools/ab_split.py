@@ -55,7 +55,7 @@ for name, lib in variants:   # each variant lays out its own split weights (MFMA
 
 
 def run(lib, name):
-    rc = lib.rvz_resnet_fwd_split(C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
+    rc = lib.rvz_resnet_fwd_split(8, C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
                                   C.c_void_p(wsp[name].data_ptr()), filters, blocks,
                                   C.c_void_p(wk.data_ptr()), C.c_void_p(lg.data_ptr()),
                                   C.c_void_p(v.data_ptr()), C.c_void_p(s))

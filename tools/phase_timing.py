@@ -35,7 +35,7 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
     wk = torch.empty(n * 192, device="cuda")
     v = torch.empty(n, device="cuda")
     for _ in range(3):
-        rc = lib.rvz_resnet_fwd_split(C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
+        rc = lib.rvz_resnet_fwd_split(8, C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
                                       C.c_void_p(ev.wsplit.data_ptr()), filters, blocks,
                                       C.c_void_p(wk.data_ptr()), C.c_void_p(lg.data_ptr()), C.c_void_p(v.data_ptr()),
                                       C.c_void_p(_lib.stream_handle()))
