@@ -5,7 +5,7 @@ set -u
 OUT=${OUT:-gpurun_out}
 TAG=${TAG:-r01}
 mkdir -p "$OUT"
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest_rc=$rc"; [ $rc -gt 1 ] && exit $rc
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
 rc=$?; echo "smoke_rc=$rc"; [ $rc -ne 0 ] && exit $rc
