@@ -1005,6 +1005,427 @@ __global__ void k_split_weights(const float* __restrict__ w, int F, int64_t tota
     }
 }
 
+// =============================================================================================
+// h2 kernel: fp32 as an exact two-part f16 split, three partial products (rvz_resnet_fwd_h2)
+//
+// Numerics. f16 carries 11 significant bits; x = x0 + x1 + r with x0 = f16(x), x1 = f16(x - x0)
+// (x - x0 is exact in fp32) and |r| <= 2^-22 |x|. Each conv product is accumulated as
+// x0w0 + x0w1 + x1w0 in ONE fp32 accumulator (v_mfma_f32_16x16x32_f16, the bf16 rate); the
+// dropped x1w1 and the residuals are <= ~2^-21 |x w|. Summed over K = 9F products with fp32
+// accumulation, the error is that of an fp32 GEMM (tools/emu_split.py: 0.8-1.5x plain fp32's
+// error against fp64 on 6x64 / 10x128 nets; tests/test_gpu_network.py measures the kernel).
+// Range: f16 is normal in [2^-14, 65504]. Weights are scaled per output channel by a power of two
+// so that the channel's max |w| lands in [2^14, 2^15) (the epilogue multiplies the accumulator by
+// the exact inverse), so every weight >= 2^-17 of its channel's max keeps 22 bits. Activations are
+// not scaled: |x| >= 2^-3 keeps 22 bits, smaller ones an absolute error <= 2^-25 (f16 subnormal
+// step of x1); |x| >= 65520 overflows to inf (a trained net's activations are far below; the
+// kernel stores 1 in work[n * 192] (the overflow word, a float) if any activation overflowed).
+// Half the MFMAs of the 3-part bf16 scheme (3 products instead of 6) and 2/3 of its LDS: 66 KB
+// per workgroup, so two workgroups share a CU and overlap one's epilogue/barrier with the
+// other's k-loop.
+//
+// LDS: act[2 buffers][2 parts][F/32 k-step planes][NBOARD*64 + 1 rows][32 halves], row
+// NBOARD*64 zero (off-board taps). A row of a plane is 4 16-byte slots; slot q of row r is stored
+// at slot q ^ ((r >> 1) & 2). A ds_read_b128 lane group of the B operand holds pixels
+// p+{0-3,12-15} at slot q and p+{4-11} at q^1 (or the mirror): per bank row class r & 3 those
+// are rows r, r+12 at q and r+4, r+8 at q^1, and bit 2 flips between r and r+4 and r+12 but not
+// r+8, so the four land in four distinct slots for every tap offset p (conflict-free, no padding).
+// The k-step and the part are immediate offsets of one address per (pixel tile, tap).
+// Wave tiles as k_resnet_split on 16x16x32: CTW = 2 channel tiles x PTW = 4 pixel tiles.
+// Weight blob (rvz_resnet_h2_weights), uint16 units:
+//   [trunk frags: layer][tap][kstep][part][ctile][lane][8]  (pre-scaled f16 parts)
+//   [H2_PAD k-steps of zeros: the prefetch past the last layer]
+//   [stem frags: part][ctile][lane][8]  (K = 27 padded to 32, k = tap*3 + ch)
+//   [inverse scales: float[1 + 2*NB][F]: stem, then the trunk layers]
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+
+#ifndef RVZ_H2_PD
+#define RVZ_H2_PD 2          // weight prefetch distance, k-steps
+#endif
+#ifndef RVZ_H2_APD
+#define RVZ_H2_APD 1         // activation prefetch distance, k-steps
+#endif
+#ifndef RVZ_H2_OCC
+#define RVZ_H2_OCC 2         // workgroups per CU the register budget is sized for
+#endif
+#define RVZ_H2_PAD 4
+static_assert(RVZ_H2_PD <= RVZ_H2_PAD, "prefetch stays inside the padded blob");
+
+constexpr int H2_K = 32, H2_TM = 16, H2_TN = 16;
+
+__host__ __device__ inline int64_t h2_layer_elems(int F) { return (int64_t)9 * F * F * 2; }
+__host__ __device__ inline int64_t h2_kstep_elems(int F) { return (int64_t)2 * F * H2_K; }
+__host__ __device__ inline int64_t h2_stem_off(int F, int NB) {
+    return 2 * NB * h2_layer_elems(F) + RVZ_H2_PAD * h2_kstep_elems(F);
+}
+__host__ __device__ inline int64_t h2_scale_off(int F, int NB) {   // uint16 units, 16-B aligned
+    return h2_stem_off(F, NB) + (int64_t)2 * F * H2_K;
+}
+__host__ __device__ inline int64_t h2_blob_elems(int F, int NB) {
+    return h2_scale_off(F, NB) + (int64_t)2 * (1 + 2 * NB) * F;
+}
+
+// x == h0 + h1 + r, |r| <= 2^-22 |x| for |x| in the f16 normal range (round to nearest even)
+__device__ __forceinline__ void split2x2(f32x2 x, uint32_t& h0, uint32_t& h1) {
+    const f16x2v a = __builtin_convertvector(x, f16x2v);
+    const f32x2 r = x - __builtin_convertvector(a, f32x2);
+    const f16x2v b = __builtin_convertvector(r, f16x2v);
+    h0 = __builtin_bit_cast(uint32_t, a);
+    h1 = __builtin_bit_cast(uint32_t, b);
+}
+__device__ __forceinline__ float h16f(uint16_t h) {
+    return (float)__builtin_bit_cast(_Float16, h);
+}
+
+template <int F, int NBOARD>
+struct CfgH {
+    static constexpr int ZROW = NBOARD * 64;
+    static constexpr int KS = F / H2_K;              // k-step planes of 32 channels
+    static constexpr int KSP = (ZROW + 1) * H2_K;    // halves per k-step plane
+    static constexpr int PLANE = KS * KSP;           // halves per part
+    static constexpr int ACT = 2 * PLANE;            // halves per buffer
+    static constexpr int XIN = NBOARD * 100 * 4;     // floats, aliased onto buffer B
+    static constexpr int BYTES = 2 * ACT * 2;
+    static constexpr int NIT = 9 * KS;
+    static constexpr int CT = F / H2_TM;
+    static_assert(XIN * 4 <= ACT * 2, "xin fits in buffer B");
+    static_assert((PLANE * 2) % 16 == 0 && (KSP * 2) % 16 == 0, "16-byte aligned planes");
+    static_assert(BYTES * RVZ_H2_OCC <= 160 * 1024, "LDS for RVZ_H2_OCC workgroups per CU");
+    // halves offset of (row, k-step plane ks, 8-channel slot q in 0..3)
+    static __device__ __forceinline__ int at(int row, int ks, int q) {
+        return ks * KSP + row * H2_K + 8 * (q ^ ((row >> 1) & 2));
+    }
+};
+
+// activation reader for the heads (join of the two parts)
+template <int F, int NBOARD>
+struct ActH2 {
+    const uint16_t* p;
+    __device__ void load8(int row, int k0, float (&v)[8]) const {
+        typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+        const int o = CfgH<F, NBOARD>::at(row, k0 / H2_K, (k0 % H2_K) >> 3);
+        const u16x8 a = *reinterpret_cast<const u16x8*>(p + o);
+        const u16x8 b = *reinterpret_cast<const u16x8*>(p + CfgH<F, NBOARD>::PLANE + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = h16f(a[j]) + h16f(b[j]);
+    }
+};
+
+template <int F, int CTW, int PTW>
+struct WaveTilesH {
+    static constexpr int CG = F / (CTW * H2_TM);
+    int ct0, px[PTW];
+    __device__ WaveTilesH(int wave, int lane) {
+        ct0 = (wave % CG) * CTW;
+        const int pt0 = (wave / CG) * PTW;
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) px[u] = (pt0 + u) * H2_TN + lane % H2_TN;
+    }
+};
+
+template <int CTW, int PTW>
+struct EpiH {
+    f32x4 bias[CTW], isc[CTW];       // per out-channel bias, inverse weight scale
+    float res[CTW][PTW][4];          // the block input (fp32) of this lane's outputs
+};
+
+template <int F, int CTW, int PTW>
+__device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __restrict__ bias,
+                                         const float* __restrict__ isc,
+                                         const WaveTilesH<F, CTW, PTW>& wt, int lane) {
+#pragma unroll
+    for (int c = 0; c < CTW; ++c) {
+        const int n = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
+        er.bias[c] = *reinterpret_cast<const f32x4*>(bias + n);
+        er.isc[c] = *reinterpret_cast<const f32x4*>(isc + n);
+    }
+}
+
+// v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
+// channels of one pixel per tile -> two 8-byte writes
+template <int F, int NBOARD, int CTW, int PTW, bool RES, bool KEEP>
+__device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
+                                            const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
+                                            const WaveTilesH<F, CTW, PTW>& wt, int lane,
+                                            bool& ovf) {
+    using C = CfgH<F, NBOARD>;
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) {
+            const int n0 = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
+            const int o = C::at(wt.px[u], n0 / H2_K, (n0 % H2_K) >> 3) + (n0 & 4);
+            u32x2 d0, d1;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                f32x2 v;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int j = 2 * hf + e;
+                    float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]);
+                    if (RES) x += er.res[c][u][j];
+                    x = fmaxf(x, 0.0f);
+                    ovf |= x >= 65520.0f;
+                    if (KEEP) er.res[c][u][j] = x;
+                    v[e] = x;
+                }
+                uint32_t h0, h1;
+                split2x2(v, h0, h1);
+                d0[hf] = h0;
+                d1[hf] = h1;
+            }
+            *reinterpret_cast<u32x2*>(out + o) = d0;
+            *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
+        }
+}
+
+__device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// the three partial products, consecutive MFMAs on different accumulators
+template <int CTW, int PTW>
+__device__ __forceinline__ void mma3(f32x4 (&acc)[CTW][PTW], const f16x8 (&a)[PTW][2],
+                                     const f16x8 (&w)[CTW][2]) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int u = 0; u < PTW; ++u)
+                acc[c][u] = mfma_h(w[c][t == 1 ? 1 : 0], a[u][t == 2 ? 1 : 0], acc[c][u]);
+}
+
+// stem conv 3 -> F as one K = 32 step (27 taps x channels + 5 zeros) on the same tile map
+template <int F, int NBOARD, int CTW, int PTW>
+__device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__ out,
+                                        const uint16_t* __restrict__ blob, const float* __restrict__ prm,
+                                        const Layout& L, int NB, int wave, int lane,
+                                        EpiH<CTW, PTW>& er, bool& ovf) {
+    const WaveTilesH<F, CTW, PTW> wt(wave, lane);
+    const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, NB));
+    load_epi(er, prm + L.stem_b, isc, wt, lane);
+    constexpr int CT = F / H2_TM;
+    const f16x8* wf = reinterpret_cast<const f16x8*>(blob + h2_stem_off(F, NB)) + wt.ct0 * 64 + lane;
+    f16x8 w[CTW][2];
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) w[c][p] = wf[(p * CT + c) * 64];
+    const int kq = 8 * (lane >> 4);
+    f16x8 a[PTW][2];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u) {
+        const int px = wt.px[u], b = px >> 6, r = (px & 63) >> 3, cc = px & 7;
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 h0, h1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            f32x2 xv;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int k = kq + 2 * i + e, t = k / 3, ch = k % 3;
+                xv[e] = k < 27 ? xin[(b * 100 + (r + t / 3) * 10 + (cc + t % 3)) * 4 + ch] : 0.0f;
+            }
+            uint32_t p0, p1;
+            split2x2(xv, p0, p1);
+            h0[i] = p0;
+            h1[i] = p1;
+        }
+        a[u][0] = __builtin_bit_cast(f16x8, h0);
+        a[u][1] = __builtin_bit_cast(f16x8, h1);
+    }
+    f32x4 acc[CTW][PTW];
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
+    mma3(acc, a, w);
+    epilogue_h2<F, NBOARD, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
+}
+
+template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS>
+__device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                        const uint16_t* __restrict__ wl,   // layer fragments
+                                        const float* __restrict__ bias,
+                                        const float* __restrict__ isc, int wave, int lane,
+                                        f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
+                                        bool& ovf) {
+    using C = CfgH<F, NBOARD>;
+    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
+    const WaveTilesH<F, CTW, PTW> wt(wave, lane);
+    load_epi(er, bias, isc, wt, lane);                // lands during the k-loop
+    const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
+    unsigned pmask[PTW];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u) {
+        const int rr = (wt.px[u] & 63) >> 3, cc = wt.px[u] & 7;
+        unsigned msk = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            if ((unsigned)(rr + t / 3 - 1) < (unsigned)BS && (unsigned)(cc + t % 3 - 1) < (unsigned)BS)
+                msk |= 1u << t;
+        pmask[u] = msk;
+    }
+    f32x4 acc[CTW][PTW];
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
+    const f16x8* wf = reinterpret_cast<const f16x8*>(wl) + wt.ct0 * 64 + lane;
+    auto load_b = [&](f16x8 (&bq)[CTW][2], int it) {
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) bq[c][p] = wf[((it * 2 + p) * CT + c) * 64];
+    };
+    auto load_a = [&](f16x8 (&aq)[PTW][2], int it) {
+        const int t = it / KS, ks = it - t * KS;
+        const int off = (t / 3 - 1) * 8 + (t % 3 - 1);
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) {
+            const int row = (pmask[u] >> t) & 1u ? wt.px[u] + off : C::ZROW;
+            const uint16_t* ap = in + C::at(row, 0, kq) + ks * C::KSP;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+                aq[u][p] = *reinterpret_cast<const f16x8*>(ap + p * C::PLANE);
+        }
+    };
+    f16x8 bq[NIT + PD][CTW][2];
+    f16x8 aq[APD + 1][PTW][2];
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) bq[d][c][p] = bc[d][c][p];
+#pragma unroll
+    for (int d = 0; d < APD; ++d) load_a(aq[d], d);
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+        if (it + APD < NIT) load_a(aq[(it + APD) % (APD + 1)], it + APD);
+        load_b(bq[it + PD], it + PD);
+        mma3(acc, aq[it % (APD + 1)], bq[it]);
+        interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
+    // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
+    epilogue_h2<F, NBOARD, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
+}
+
+template <int F, int NBOARD, int CTW, int PTW, int BS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RVZ_H2_OCC, RVZ_H2_OCC)))
+void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
+                 Layout L, const uint16_t* __restrict__ blob, int n_blocks,
+                 float* __restrict__ work) {
+    using C = CfgH<F, NBOARD>;
+    using WT = WaveTilesH<F, CTW, PTW>;
+    static_assert(WT::CG * (NBOARD * 64 / (PTW * H2_TN)) == 4, "4 waves");
+    constexpr int NTHR = 256;
+    __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
+    uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* actB = actA + C::ACT;
+    float* xin = reinterpret_cast<float*>(actB);     // free until the first conv writes B
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g0 = blockIdx.x * NBOARD;
+    bool ovf = false;
+
+    // zero rows of both buffers, both parts, every k-step plane (4 * KS planes of KSP)
+    for (int i = tid; i < 4 * C::KS * H2_K; i += NTHR) {
+        const int plane = i / H2_K, k = i % H2_K;
+        actA[plane * C::KSP + C::ZROW * H2_K + k] = 0;
+    }
+    f16x8 bc[RVZ_H2_PD][CTW][2];
+    if (n_blocks > 0) {
+        const f16x8* wf = reinterpret_cast<const f16x8*>(blob) + WT(wave, lane).ct0 * 64 + lane;
+#pragma unroll
+        for (int s = 0; s < RVZ_H2_PD; ++s)
+#pragma unroll
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) bc[s][c][p] = wf[((s * 2 + p) * C::CT + c) * 64];
+    }
+    load_input<NBOARD, BS>(x, n_boards, g0, xin, tid, NTHR);
+    __syncthreads();
+    EpiH<CTW, PTW> er;
+    stem_h2<F, NBOARD, CTW, PTW>(xin, actA, blob, prm, L, n_blocks, wave, lane, er, ovf);
+    __syncthreads();
+    const int64_t LW = h2_layer_elems(F);
+    const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
+    for (int blk = 0; blk < n_blocks; ++blk) {
+        const int l1 = 2 * blk, l2 = 2 * blk + 1;
+        conv_h2<F, NBOARD, CTW, PTW, false, BS>(actA, actB, blob + l1 * LW,
+                                                prm + L.res_b + (size_t)l1 * F, isc + l1 * F,
+                                                wave, lane, bc, er, ovf);
+        __syncthreads();
+        conv_h2<F, NBOARD, CTW, PTW, true, BS>(actB, actA, blob + l2 * LW,
+                                               prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
+                                               wave, lane, bc, er, ovf);
+        __syncthreads();
+    }
+    head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, reinterpret_cast<float*>(actB), prm, L,
+                                    HeadsGlobal{work, g0, n_boards}, tid);
+    if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
+}
+
+// per (layer, out-channel) wave: scale = 2^(14 - floor(log2 max|w|)), split the scaled weights
+// into the fragment layout, store 1/scale. Layer -1 (blockIdx.y == 0) is the stem.
+__global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm, Layout L, int F,
+                                                   int NB, uint16_t* __restrict__ blob) {
+    const int n = blockIdx.x, lyr = (int)blockIdx.y - 1, lane = threadIdx.x;
+    const int CT = F / H2_TM, KS = F / H2_K;
+    const int cnt = lyr < 0 ? 27 : 9 * F;
+    auto wget = [&](int i) -> float {   // i = tap*F + k (trunk) or k (stem)
+        if (lyr < 0) return prm[L.stem_w + (int64_t)n * 27 + i];
+        const int t = i / F, k = i % F;
+        return prm[L.res_w + (((int64_t)lyr * 9 + t) * F + n) * F + k];
+    };
+    float m = 0.0f;
+    for (int i = lane; i < cnt; i += 64) m = fmaxf(m, fabsf(wget(i)));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    int e = 0;
+    if (m > 0.0f) {
+        frexpf(m, &e);                         // m = f * 2^e, f in [0.5, 1): floor(log2 m) = e - 1
+        e = 14 - (e - 1);
+        e = e < -100 ? -100 : (e > 100 ? 100 : e);
+    }
+    const float sc = ldexpf(1.0f, e);
+    float* isc = reinterpret_cast<float*>(blob + h2_scale_off(F, NB));
+    if (lane == 0) isc[(lyr + 1) * F + n] = ldexpf(1.0f, -e);
+    const int ct = n / H2_TM;
+    if (lyr < 0) {                             // stem: [part][ct][lane][8], k < 32
+        uint16_t* o = blob + h2_stem_off(F, NB);
+        if (lane < 32) {
+            const int k = lane, ln = (k / 8) * H2_TM + n % H2_TM;
+            const float w = k < 27 ? wget(k) * sc : 0.0f;
+            const _Float16 h0 = (_Float16)w;
+            const _Float16 h1 = (_Float16)(w - (float)h0);
+            o[((0 * CT + ct) * 64 + ln) * 8 + k % 8] = __builtin_bit_cast(uint16_t, h0);
+            o[((1 * CT + ct) * 64 + ln) * 8 + k % 8] = __builtin_bit_cast(uint16_t, h1);
+        }
+        return;
+    }
+    for (int i = lane; i < cnt; i += 64) {
+        const int t = i / F, k = i % F, ks = k / H2_K, ln = ((k % H2_K) / 8) * H2_TM + n % H2_TM;
+        const float w = wget(i) * sc;
+        const _Float16 h0 = (_Float16)w;
+        const _Float16 h1 = (_Float16)(w - (float)h0);
+        const int64_t base = (((int64_t)lyr * 9 + t) * KS + ks) * 2;
+        blob[(((base + 0) * CT + ct) * 64 + ln) * 8 + k % 8] = __builtin_bit_cast(uint16_t, h0);
+        blob[(((base + 1) * CT + ct) * 64 + ln) * 8 + k % 8] = __builtin_bit_cast(uint16_t, h1);
+    }
+}
+
 }  // namespace
 
 template <int BS>
@@ -1018,6 +1439,18 @@ static void launch_trunk(const float* x, int32_t n, const float* params, const u
     else
         hipLaunchKernelGGL((k_resnet_split<SplitShape, 128, 1, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW, BS>),
                            dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
+}
+
+template <int BS>
+static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
+                            int32_t filters, int32_t blocks, float* work, hipStream_t s) {
+    const Layout L = make_layout(filters, blocks, BS);
+    if (filters == 64)
+        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, BS>), dim3((n + 1) / 2), dim3(256), 0, s, x, n,
+                           params, L, blob, blocks, work);
+    else
+        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, BS>), dim3(n), dim3(256), 0, s, x, n, params,
+                           L, blob, blocks, work);
 }
 
 
@@ -1088,7 +1521,8 @@ int rvz_resnet_split_weights(const float* params, int32_t filters, int32_t block
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
-int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192; }
+// + 4 floats: word n*192 is the h2 kernel's sticky activation-overflow flag
+int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192 + 4; }
 
 int rvz_resnet_trunk_split(int32_t board, const float* x, int32_t n, const float* params,
                            const uint16_t* wsplit, int32_t filters, int32_t blocks, float* work,
@@ -1129,6 +1563,49 @@ int rvz_resnet_fwd_split(int32_t board, const float* x, int32_t n, const float* 
     if (!logits || !value) return RVZ_EINVAL;
     const int rc =
         rvz_resnet_trunk_split(board, x, n, params, wsplit, filters, blocks, work, stream);
+    if (rc != RVZ_OK) return rc;
+    return rvz_resnet_heads_fc(board, work, n, params, filters, blocks, logits, value, stream);
+}
+
+int64_t rvz_resnet_h2_size(int32_t filters, int32_t blocks) {
+    if ((filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
+    return h2_blob_elems(filters, blocks);
+}
+
+int rvz_resnet_h2_weights(const float* params, int32_t filters, int32_t blocks, uint16_t* blob,
+                          void* stream) {
+    if (!params || !blob || (filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
+    if (((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    const Layout L = make_layout(filters, blocks);
+    // the prefetch padding after the last layer reads zeros
+    if (hipMemsetAsync(blob + 2 * blocks * h2_layer_elems(filters), 0,
+                       RVZ_H2_PAD * h2_kstep_elems(filters) * 2, s) != hipSuccess)
+        return RVZ_EHIP;
+    hipLaunchKernelGGL(k_h2_weights, dim3(filters, 1 + 2 * blocks), dim3(64), 0, s, params, L,
+                       (int)filters, (int)blocks, blob);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* params,
+                        const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
+                        void* stream) {
+    if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
+        (filters != 64 && filters != 128))
+        return RVZ_EINVAL;
+    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    hipStream_t s = (hipStream_t)stream;
+    if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, s);
+    else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, s);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_resnet_fwd_h2(int32_t board, const float* x, int32_t n, const float* params,
+                      const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
+                      float* logits, float* value, void* stream) {
+    if (!logits || !value) return RVZ_EINVAL;
+    const int rc = rvz_resnet_trunk_h2(board, x, n, params, blob, filters, blocks, work, stream);
     if (rc != RVZ_OK) return rc;
     return rvz_resnet_heads_fc(board, work, n, params, filters, blocks, logits, value, stream);
 }

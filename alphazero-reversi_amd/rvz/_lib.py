@@ -74,6 +74,12 @@ SIGNATURES = {
                                          _P, _P]),
     "rvz_resnet_heads_fc": (C.c_int, [C.c_int32, _P, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P,
                                       _P]),
+    "rvz_resnet_h2_size": (C.c_int64, [C.c_int32, C.c_int32]),
+    "rvz_resnet_h2_weights": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
+    "rvz_resnet_trunk_h2": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32,
+                                      _P, _P]),
+    "rvz_resnet_fwd_h2": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32, _P,
+                                    _P, _P, _P]),
     "rvz_resnet_fwd_split": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32, _P,
                                        _P, _P, _P]),
 }

@@ -151,25 +151,27 @@ class LeafEvaluator:
         net = net.eval()
         dev = torch.device(device) if device is not None else next(net.parameters()).device
         self.dtype, self.device = dtype, dev
-        # kernel: the whole forward in one rvz kernel (fp32, 8x8, 64/128 filters) —
-        #   "split" = fp32 emulated exactly-split on the bf16 MFMA (rvz_resnet_fwd_split),
-        #   "resnet" = the f32-input MFMA (rvz_resnet_fwd_f32);
-        # "miopen" = PyTorch convs (+ the fused epilogue); "auto" = split where it applies
+        # kernel: the whole forward in one rvz kernel (fp32, 8x8 or 6x6, 64/128 filters) —
+        #   "h2" = fp32 as a two-part f16 split, 3 products, on the f16 MFMA (rvz_resnet_fwd_h2),
+        #   "split" = fp32 as a three-part bf16 split, 6 products, on the bf16 MFMA
+        #             (rvz_resnet_fwd_split),
+        #   "resnet" = the f32-input MFMA (rvz_resnet_fwd_f32, 8x8 only);
+        # "miopen" = PyTorch convs (+ the fused epilogue); "auto" = h2 where it applies
         self.n_blocks, self.filters = len(net.res_blocks), net.num_filters
         self.board_size = net.board_size
         split_ok = (dev.type == "cuda" and dtype == torch.float32 and net.board_size in (6, 8)
                     and net.num_filters in (64, 128))
-        if kernel not in ("auto", "split", "resnet", "miopen"):
+        if kernel not in ("auto", "h2", "split", "resnet", "miopen"):
             raise ValueError(f"unknown kernel {kernel!r}")
-        if kernel == "split" and not split_ok:
-            raise ValueError("the split resnet kernel needs fp32, 8x8 or 6x6, 64 or 128 filters, "
-                             "a GPU")
+        if kernel in ("h2", "split") and not split_ok:
+            raise ValueError(f"the {kernel} resnet kernel needs fp32, 8x8 or 6x6, 64 or 128 "
+                             "filters, a GPU")
         if kernel == "resnet" and not (split_ok and net.board_size == 8):
             raise ValueError("the f32 resnet kernel needs fp32, 8x8, 64 or 128 filters, a GPU")
         if kernel == "auto":
-            kernel = "split" if split_ok else "miopen"
+            kernel = "h2" if split_ok else "miopen"
         self.kernel = kernel
-        self.use_resnet = kernel in ("split", "resnet")
+        self.use_resnet = kernel in ("h2", "split", "resnet")
         self._outs = {}
         if self.use_resnet:
             from . import _lib
@@ -180,6 +182,12 @@ class LeafEvaluator:
             if want != self.params.numel():
                 raise _lib.RvzError(f"packed params {self.params.numel()} != layout {want}")
             self.wsplit = None
+            if kernel == "h2":
+                n = lib.rvz_resnet_h2_size(self.filters, self.n_blocks)
+                self.wsplit = torch.empty(n, dtype=torch.int16, device=dev)
+                _lib.check(lib.rvz_resnet_h2_weights(
+                    self.params.data_ptr(), self.filters, self.n_blocks, self.wsplit.data_ptr(),
+                    _lib.stream_handle(dev)), None, "rvz_resnet_h2_weights")
             if kernel == "split":
                 n = lib.rvz_resnet_split_size(self.filters, self.n_blocks)
                 self.wsplit = torch.empty(max(n, 8), dtype=torch.int16, device=dev)
@@ -242,10 +250,15 @@ class LeafEvaluator:
         if outs is None:   # fixed per batch size: stable addresses under HIP-graph capture
             outs = (torch.empty(n, self.board_size ** 2 + 1, device=self.device),
                     torch.empty(n, device=self.device),
-                    torch.empty(max(1, _lib.load().rvz_resnet_work_size(n)), device=self.device))
+                    torch.zeros(_lib.load().rvz_resnet_work_size(n), device=self.device))
             self._outs[n] = outs
         logits, value, work = outs
-        if self.wsplit is not None:
+        if self.kernel == "h2":
+            _lib.check(_lib.load().rvz_resnet_fwd_h2(
+                self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
+                self.filters, self.n_blocks, work.data_ptr(), logits.data_ptr(),
+                value.data_ptr(), _lib.stream_handle(x.device)), None, "rvz_resnet_fwd_h2")
+        elif self.wsplit is not None:
             _lib.check(_lib.load().rvz_resnet_fwd_split(
                 self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
                 self.filters, self.n_blocks, work.data_ptr(), logits.data_ptr(),
@@ -258,25 +271,38 @@ class LeafEvaluator:
         return logits, value
 
     def trunk_only(self, x: torch.Tensor):
-        """The split path's first launch alone (rvz_resnet_trunk_split: stem, residual tower,
-        1x1 head convs -> the workspace); bench.py times the dominant kernel with it."""
+        """The h2 / split path's first launch alone (rvz_resnet_trunk_h2 / _split: stem,
+        residual tower, 1x1 head convs -> the workspace); bench.py times the dominant kernel
+        with it."""
         from . import _lib
         if self.wsplit is None:
-            raise _lib.RvzError("trunk_only needs kernel='split'")
+            raise _lib.RvzError("trunk_only needs kernel='h2' or 'split'")
         if x.shape[0] not in self._outs:
             self(x)                                # allocates the per-batch buffers
         work = self._outs[x.shape[0]][2]
-        _lib.check(_lib.load().rvz_resnet_trunk_split(
-            self.board_size, x.data_ptr(), x.shape[0], self.params.data_ptr(),
-            self.wsplit.data_ptr(), self.filters, self.n_blocks, work.data_ptr(),
-            _lib.stream_handle(x.device)), None, "rvz_resnet_trunk_split")
+        fn = (_lib.load().rvz_resnet_trunk_h2 if self.kernel == "h2"
+              else _lib.load().rvz_resnet_trunk_split)
+        _lib.check(fn(self.board_size, x.data_ptr(), x.shape[0], self.params.data_ptr(),
+                      self.wsplit.data_ptr(), self.filters, self.n_blocks, work.data_ptr(),
+                      _lib.stream_handle(x.device)), None, "rvz_resnet_trunk")
+
+    @property
+    def trunk_kernel_name(self) -> str:
+        return {"h2": "k_resnet_h2", "split": "k_resnet_split"}.get(self.kernel, "")
+
+    def overflowed(self) -> bool:
+        """h2 only: True if any activation of any call so far reached the f16 range limit
+        (65520) — the outputs of that call are then not valid (synchronises)."""
+        return any(bool(w[-4].item() != 0) for _, _, w in self._outs.values()) \
+            if self.kernel == "h2" else False
 
     def mfma_flops_per_row(self) -> int:
-        """FLOPs the split trunk kernel executes on the bf16 matrix cores per board: six partial
-        products per fp32 product, stem K padded 27 -> 32, over the 8x8 pixel grid (a 6x6 board
-        is computed embedded in it)."""
+        """FLOPs the trunk kernel executes on the 16-bit matrix cores per board, stem K padded
+        27 -> 32, over the 8x8 pixel grid (a 6x6 board is computed embedded in it): three
+        partial products per fp32 product for h2 (f16 MFMA), six for split (bf16 MFMA)."""
         cells, f = 64, self.filters
-        return 6 * 2 * cells * f * (32 + 2 * self.n_blocks * 9 * f)
+        terms = 3 if self.kernel == "h2" else 6
+        return terms * 2 * cells * f * (32 + 2 * self.n_blocks * 9 * f)
 
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):

@@ -59,8 +59,11 @@ def parse():
     ap.add_argument("--board", type=int, default=None)
     ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--nn-kernel", choices=["auto", "split", "resnet", "miopen"], default="auto",
-                    help="leaf evaluator: split (fp32 as exact 3xbf16 split, MFMA), resnet (f32 MFMA), miopen")
+    ap.add_argument("--nn-kernel", choices=["auto", "h2", "split", "resnet", "miopen"],
+                    default="auto",
+                    help="leaf evaluator: h2 (fp32 as a 2-part f16 split, 3 products, MFMA; the "
+                         "auto choice), split (3-part bf16 split, 6 products), resnet (f32 MFMA), "
+                         "miopen")
     ap.add_argument("--instrument-plies", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,7 +118,7 @@ def instrumented(run, eng, ev, plies):
     torch.cuda.synchronize(eng.device)
     ms = {"step": t["step"][0], "act": t["act"][0], "nn": a.elapsed_time(b) / 10}
     n = {"step": t["step"][1], "act": t["act"][1], "nn": nn_calls}
-    if getattr(ev, "kernel", None) == "split":   # the trunk launch alone: the dominant kernel
+    if getattr(ev, "kernel", None) in ("h2", "split"):   # the trunk launch alone: the dominant kernel
         ev.trunk_only(eng.leaf_x)
         a.record(stream)
         for _ in range(10):
@@ -241,9 +244,9 @@ def main():
     nn_tflops = nn_flops / (ms["nn"] * 1e-3) / 1e12
     nn_per_ply = n["nn"] / max(1, args.instrument_plies)
     split = "nn_trunk" in ms
-    if split:   # roofline of the NN trunk kernel: executed bf16-MFMA FLOPs per launch / duration
+    if split:   # roofline of the NN trunk kernel: executed 16-bit MFMA FLOPs per launch / duration
         mf = ev.mfma_flops_per_row() * args.games
-        nn_roof = {"kernel": "k_resnet_split", "bound": "mfma",
+        nn_roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
                    "achieved": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12, 2),
                    "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
                    "frac": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
@@ -277,14 +280,17 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u64 rules + f32 NN" + (" (exact 3xbf16 split on MFMA)" if split else ""),
+            "dtype": "u64 rules + f32 NN" + ({"h2": " (fp32 as 2-part f16 split on MFMA)",
+                                               "split": " (fp32 as 3-part bf16 split on MFMA)"}
+                                              .get(ev.kernel, "") if split else ""),
             "data": "synthetic (start position, per-game seeds, random-init net)",
             "config": {"workload": f"{args.config}: {args.games} games/GPU x {args.sims} sims, "
                                    f"{args.blocks}x{args.filters} ResNet, {args.board}x{args.board}",
                        "games_per_gpu": args.games, "global_games": args.games * world,
                        "sims": args.sims, "batch": args.batch,
                        "nn": f"{args.blocks}x{args.filters}", "nn_dtype": args.nn_dtype,
-                       "nn_kernel": {"split": "rvz_resnet_fwd_split", "resnet": "rvz_resnet_fwd_f32"}
+                       "nn_kernel": {"h2": "rvz_resnet_fwd_h2", "split": "rvz_resnet_fwd_split",
+                                     "resnet": "rvz_resnet_fwd_f32"}
                        .get(getattr(ev, "kernel", ""), "miopen+rvz_nn_bias_act"),
                        "graph": not args.no_graph, "parallelism": f"games sharded x{world}"},
             # the dominant kernel of a ply (by time per ply) carries "roofline"; the other side

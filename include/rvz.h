@@ -173,6 +173,24 @@ int rvz_resnet_heads_fc(int32_t board, const float *work, int32_t n, const float
                         int32_t filters, int32_t blocks, float *logits, float *value,
                         void *hip_stream);
 
+/* The same forward, fp32 emulated on the f16 MFMA with two parts per operand (the default leaf
+ * evaluator): x = x0 + x1 (f16 each, 22 significant bits), weights pre-scaled per output channel
+ * by a power of two, the three partial products x0w0 + x0w1 + x1w0 accumulated in one fp32
+ * accumulator (error of an fp32 GEMM; see csrc/rvz_resnet.hip k_resnet_h2). Boards 8 and 6.
+ * blob: rvz_resnet_h2_weights' output (scaled f16 parts + inverse scales, once per parameter
+ * update), rvz_resnet_h2_size(filters, blocks) uint16 elements, 16-byte aligned.
+ * work: rvz_resnet_work_size(n) floats; work[n * 192] is set to 1 (never cleared by the kernel)
+ * if an activation reached the f16 range limit 65520, i.e. the outputs are not valid. */
+int64_t rvz_resnet_h2_size(int32_t filters, int32_t blocks);
+int rvz_resnet_h2_weights(const float *params, int32_t filters, int32_t blocks, uint16_t *blob,
+                          void *hip_stream);
+int rvz_resnet_fwd_h2(int32_t board, const float *x, int32_t n, const float *params,
+                      const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
+                      float *logits, float *value, void *hip_stream);
+int rvz_resnet_trunk_h2(int32_t board, const float *x, int32_t n, const float *params,
+                        const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
+                        void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -101,22 +101,22 @@ def test_split_kernel_6x6_matches_module(blocks, filters, n):
     x = (torch.rand(n, 3, 6, 6, device="cuda") > 0.6).float()
     with torch.no_grad():
         lr, vr = net(x)
-    ev = rvz.LeafEvaluator(net)
-    assert ev.kernel == "split"
-    l, v = ev(x)
-    torch.cuda.synchronize()
-    assert l.shape == (n, 37)
-    scale = lr.abs().max().item()
-    assert (l - lr).abs().max().item() <= 2e-5 * scale
-    assert (v - vr).abs().max().item() <= 2e-3
+    assert rvz.LeafEvaluator(net).kernel == "h2"
+    for kern in ("h2", "split"):
+        l, v = rvz.LeafEvaluator(net, kernel=kern)(x)
+        torch.cuda.synchronize()
+        assert l.shape == (n, 37)
+        scale = lr.abs().max().item()
+        assert (l - lr).abs().max().item() <= 2e-5 * scale, kern
+        assert (v - vr).abs().max().item() <= 2e-3, kern
 
 
-@pytest.mark.parametrize("kernel", ["resnet", "split"])
+@pytest.mark.parametrize("kernel", ["resnet", "split", "h2"])
 @pytest.mark.parametrize("blocks,filters,n", [(6, 64, 4096), (10, 128, 515), (1, 64, 3), (0, 128, 2)])
 def test_resnet_kernel_matches_module(kernel, blocks, filters, n):
-    """rvz_resnet_fwd_f32 (f32 MFMA) and rvz_resnet_fwd_split (fp32 split over bf16 MFMA), whole
-    forward, vs the nn.Module (fp32): fp32-class arithmetic, different summation order; odd batch
-    sizes cover the partial last workgroup."""
+    """rvz_resnet_fwd_f32 (f32 MFMA), rvz_resnet_fwd_split (fp32 as 3 bf16 parts) and
+    rvz_resnet_fwd_h2 (fp32 as 2 f16 parts), whole forward, vs the nn.Module (fp32): fp32-class
+    arithmetic, different summation order; odd batch sizes cover the partial last workgroup."""
     import rvz
     net = _bn_net(blocks, filters)
     x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
@@ -133,8 +133,9 @@ def test_resnet_kernel_matches_module(kernel, blocks, filters, n):
 
 @pytest.mark.parametrize("blocks,filters,n", [(6, 64, 512), (10, 128, 128)])
 def test_split_error_is_fp32_class(blocks, filters, n):
-    """Error against an fp64 evaluation of the same module: the split kernel's must be of the
-    order of the fp32 paths' (f32 MFMA kernel, PyTorch fp32) — not bf16's (~1e-3 relative)."""
+    """Error against an fp64 evaluation of the same module: the split kernels' (3 bf16 parts, 2
+    f16 parts) must be of the order of the fp32 paths' (f32 MFMA kernel, PyTorch fp32) — not
+    bf16's (~1e-3 relative). tools/emu_split.py predicts h2 at 0.8-1.5x plain fp32."""
     import rvz
     net = _bn_net(blocks, filters, seed=5)
     x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
@@ -143,17 +144,18 @@ def test_split_error_is_fp32_class(blocks, filters, n):
         net.float().cuda()
         lm, vm = net(x)
     err = {}
-    for kern in ("resnet", "split"):
+    for kern in ("resnet", "split", "h2"):
         l, v = rvz.LeafEvaluator(net, kernel=kern)(x)
         err[kern] = (l.double().cpu() - l64).abs().max().item()
     err["module"] = (lm.double().cpu() - l64).abs().max().item()
     scale = l64.abs().max().item()
     fp32 = max(err["resnet"], err["module"])
-    assert err["split"] <= 4 * fp32 + 1e-7 * scale, (err, scale)
-    assert err["split"] <= 1e-5 * scale, (err, scale)
+    for kern in ("split", "h2"):
+        assert err[kern] <= 4 * fp32 + 1e-7 * scale, (kern, err, scale)
+        assert err[kern] <= 1e-5 * scale, (kern, err, scale)
 
 
-@pytest.mark.parametrize("kernel", ["split", "resnet", "miopen"])
+@pytest.mark.parametrize("kernel", ["h2", "split", "resnet", "miopen"])
 def test_evaluator_matches_reference_outputs(kernel):
     """Every NN call of the reference's S=800 6x64 self-play fixture (1,499 leaf positions):
     the GPU evaluator's softmax rows and values against the reference's own recorded outputs
@@ -175,3 +177,50 @@ def test_evaluator_matches_reference_outputs(kernel):
     dv = np.abs(v.cpu().numpy() - value).max()
     assert dp <= 2e-5 and dv <= 5e-4, (dp, dv)
     assert (p.argmax(1) == probs.argmax(1)).mean() > 0.99
+
+
+def test_h2_overflow_flag():
+    """h2 keeps activations as two f16 parts: an activation >= 65520 cannot be represented. The
+    kernel raises the sticky overflow word instead of returning silently wrong outputs."""
+    import rvz
+    net = _bn_net(2, 64, seed=6)
+    x = (torch.rand(64, 3, 8, 8, device="cuda") > 0.6).float()
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    ev(x)
+    assert not ev.overflowed()
+    with torch.no_grad():
+        net.bn.bias.fill_(1e5)            # stem output ~1e5 > the f16 range
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    ev(x)
+    assert ev.overflowed()
+
+
+def test_h2_weight_blob():
+    """rvz_resnet_h2_weights: every fragment element is the f16 split of the scaled weight
+    (w * 2^s == h0 + h1 up to 2^-22 relative), max |w| of each channel scaled into [2^14, 2^15),
+    inverse scales exact powers of two."""
+    import rvz
+    net = _bn_net(1, 64, seed=7)
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    blob = ev.wsplit.cpu().numpy().view(np.uint16)
+    F, NB, K, TM = 64, 1, 32, 16
+    layer = 9 * F * F * 2
+    stem_off = 2 * NB * layer + 4 * 2 * F * K
+    sc_off = stem_off + 2 * F * K
+    isc = blob[sc_off:sc_off + 2 * (1 + 2 * NB) * F].view(np.float32).reshape(1 + 2 * NB, F)
+    assert np.all(np.log2(isc) == np.round(np.log2(isc)))
+    prm = ev.params.cpu().numpy()
+    from rvz.network import _fold
+    w1, _ = _fold(net.res_blocks[0].conv1, net.res_blocks[0].bn1)
+    w1 = w1.cpu().numpy()                                     # [n][k][3][3]
+    frag = blob[:layer].view(np.float16).reshape(9, F // K, 2, F // TM, 64, 8).astype(np.float64)
+    # rebuild w[t][n][k] from the fragments: lane = ((k % K) / 8) * TM + n % TM
+    t, n, k = np.meshgrid(np.arange(9), np.arange(F), np.arange(F), indexing="ij")
+    ln = ((k % K) // 8) * TM + n % TM
+    h = frag[t, k // K, :, n // TM, ln, k % 8]                # [..., part]
+    rebuilt = (h[..., 0] + h[..., 1]) * isc[1][n]
+    ref = w1.transpose(2, 3, 0, 1).reshape(9, F, F).astype(np.float64)
+    assert np.abs(rebuilt - ref).max() <= 2 ** -21 * np.abs(ref).max()
+    scaled_max = np.abs(ref).reshape(9, F, F).max(axis=(0, 2)) / isc[1]
+    assert np.all((scaled_max >= 2 ** 14) & (scaled_max < 2 ** 15))
+    assert prm.dtype == np.float32

@@ -47,6 +47,11 @@ def conv_scheme(x, w, scheme, act_log2):
         ws = parts(w * sw.view(-1, 1, 1, 1), torch.float16, 2)
         hi_t = [(0, 0)]
         lo_t = [(0, 1), (1, 0)] + ([(1, 1)] if scheme == "f16x2_4" else [])
+        if scheme == "f16x2_1acc":   # one fp32 accumulator for all three products
+            xa = torch.cat([xs[0], xs[0], xs[1]], 1).float()
+            wa = torch.cat([ws[0], ws[1], ws[0]], 1).float()
+            y = F.conv2d(xa, wa, padding=1).double()
+            return y / (sx * sw.view(1, -1, 1, 1))
     conv = lambda a, b: F.conv2d(a.float(), b.float(), padding=1)  # fp32 accumulation  # noqa
     hi = sum(conv(xs[i], ws[j]) for i, j in hi_t)
     lo = torch.zeros_like(hi)
@@ -99,7 +104,7 @@ def main():
         l64, v64, h64 = forward(net, x, "exact64")
         scale = l64.abs().max().item()
         print(f"net {blocks}x{filters}, n={n}: logit scale {scale:.3g}, trunk max {h64.max():.3g}")
-        for s in ("fp32", "bf16x3_6", "f16x2_3", "f16x2_4"):
+        for s in ("fp32", "bf16x3_6", "f16x2_3", "f16x2_4", "f16x2_1acc"):
             l, v, h = forward(net, x, s, act)
             print(f"{s:9s} max|dl|/scale {((l - l64).abs().max() / scale).item():.3e}  "
                   f"max|dv| {(v - v64).abs().max().item():.3e}  "
