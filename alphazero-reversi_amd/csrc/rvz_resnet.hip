@@ -264,38 +264,40 @@ struct HeadsGlobal {     // hpv rows in the global workspace of rvz_resnet_fwd_s
     }
 };
 
-// heads, part 2 (in-kernel form): policy fc (128 -> 65), value fc1 (64 -> 256, ReLU), value fc2
-// (256 -> 1) + tanh, for the NBOARD boards of a workgroup; hpv in LDS
-template <int NBOARD, int NTHR>
+// heads, part 2 (in-kernel form): policy fc (2 cells -> cells + 1), value fc1 (cells -> 256,
+// ReLU), value fc2 (256 -> 1) + tanh, for the NBOARD boards of a workgroup; hpv in LDS (rows of
+// 192: policy planes, then the value plane)
+template <int NBOARD, int NTHR, int BS = 8>
 __device__ __forceinline__ void head_fcs(const float* hpv, float* h1,
                                          const float* __restrict__ prm, const Layout& L, int g0,
                                          int n_boards, float* __restrict__ logits,
                                          float* __restrict__ value, int tid) {
+    constexpr int CELLS = BS * BS, POUT = CELLS + 1, PIN = 2 * CELLS, ROWS = POUT + 256;
     const int lane = tid & 63;
     // thread per output row, f32x4 loads
-    for (int o = tid; o < NBOARD * (65 + 256); o += NTHR) {
-        const int b = o / 321, rem = o % 321;
+    for (int o = tid; o < NBOARD * ROWS; o += NTHR) {
+        const int b = o / ROWS, rem = o % ROWS;
         const int g = g0 + b;
-        if (rem < 65) {
-            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.pfc_w + rem * 128);
+        if (rem < POUT) {
+            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.pfc_w + rem * PIN);
             const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192);
             float acc = prm[L.pfc_b + rem];
 #pragma unroll 16
-            for (int i = 0; i < 32; ++i) {
+            for (int i = 0; i < PIN / 4; ++i) {
                 const f32x4 w = wr[i], v = in[i];
                 acc = fmaf(v[0], w[0], acc);
                 acc = fmaf(v[1], w[1], acc);
                 acc = fmaf(v[2], w[2], acc);
                 acc = fmaf(v[3], w[3], acc);
             }
-            if (g < n_boards) logits[(size_t)g * 65 + rem] = acc;
+            if (g < n_boards) logits[(size_t)g * POUT + rem] = acc;
         } else {
-            const int u = rem - 65;
-            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + u * 64);
-            const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192 + 128);
+            const int u = rem - POUT;
+            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + u * CELLS);
+            const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192 + PIN);
             float acc = prm[L.vfc1_b + u];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < CELLS / 4; ++i) {
                 const f32x4 w = wr[i], v = in[i];
                 acc = fmaf(v[0], w[0], acc);
                 acc = fmaf(v[1], w[1], acc);
@@ -1024,12 +1026,14 @@ __global__ void k_split_weights(const float* __restrict__ w, int F, int64_t tota
 // per workgroup, so two workgroups share a CU and overlap one's epilogue/barrier with the
 // other's k-loop.
 //
-// LDS: act[2 buffers][2 parts][F/32 k-step planes][NBOARD*64 + 1 rows][32 halves], row
-// NBOARD*64 zero (off-board taps). A row of a plane is 4 16-byte slots; slot q of row r is stored
-// at slot q ^ ((r >> 1) & 2). A ds_read_b128 lane group of the B operand holds pixels
-// p+{0-3,12-15} at slot q and p+{4-11} at q^1 (or the mirror): per bank row class r & 3 those
-// are rows r, r+12 at q and r+4, r+8 at q^1, and bit 2 flips between r and r+4 and r+12 but not
-// r+8, so the four land in four distinct slots for every tap offset p (conflict-free, no padding).
+// LDS: act[2 buffers][2 parts][F/32 k-step planes][NBOARD*64 + 8 rows][32 halves]; rows
+// NBOARD*64 .. +7 are zero. A row of a plane is 4 16-byte slots; slot q of row r is stored at
+// slot q ^ ((r >> 1) & 3). An off-board tap of target row r reads zero row NBOARD*64 + (r & 7),
+// which has r's bank placement. Bank analysis (ds_read_b128 lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} +32; ds_write_b64 groups of 16 contiguous lanes; MI355X_MICROARCH.md §LDS),
+// checked exhaustively over every tap, tile and both board sizes by tools/lds_banks.py: the B
+// operand reads are conflict-free (4 LDS cycles per read), the epilogue's 8-byte writes 2-way,
+// the minimum for 16 pixels x one channel quad in 64-byte rows.
 // The k-step and the part are immediate offsets of one address per (pixel tile, tap).
 // Wave tiles as k_resnet_split on 16x16x32: CTW = 2 channel tiles x PTW = 4 pixel tiles.
 // Weight blob (rvz_resnet_h2_weights), uint16 units:
@@ -1083,7 +1087,7 @@ template <int F, int NBOARD>
 struct CfgH {
     static constexpr int ZROW = NBOARD * 64;
     static constexpr int KS = F / H2_K;              // k-step planes of 32 channels
-    static constexpr int KSP = (ZROW + 1) * H2_K;    // halves per k-step plane
+    static constexpr int KSP = (ZROW + 8) * H2_K;    // halves per k-step plane
     static constexpr int PLANE = KS * KSP;           // halves per part
     static constexpr int ACT = 2 * PLANE;            // halves per buffer
     static constexpr int XIN = NBOARD * 100 * 4;     // floats, aliased onto buffer B
@@ -1095,7 +1099,7 @@ struct CfgH {
     static_assert(BYTES * RVZ_H2_OCC <= 160 * 1024, "LDS for RVZ_H2_OCC workgroups per CU");
     // halves offset of (row, k-step plane ks, 8-channel slot q in 0..3)
     static __device__ __forceinline__ int at(int row, int ks, int q) {
-        return ks * KSP + row * H2_K + 8 * (q ^ ((row >> 1) & 2));
+        return ks * KSP + row * H2_K + 8 * (q ^ ((row >> 1) & 3));
     }
 };
 
@@ -1200,20 +1204,28 @@ __device__ __forceinline__ void mma3(f32x4 (&acc)[CTW][PTW], const f16x8 (&a)[PT
 
 // stem conv 3 -> F as one K = 32 step (27 taps x channels + 5 zeros) on the same tile map
 template <int F, int NBOARD, int CTW, int PTW>
-__device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__ out,
-                                        const uint16_t* __restrict__ blob, const float* __restrict__ prm,
-                                        const Layout& L, int NB, int wave, int lane,
-                                        EpiH<CTW, PTW>& er, bool& ovf) {
+__device__ __forceinline__ void stem_h2_load(const uint16_t* __restrict__ blob,
+                                             const float* __restrict__ prm, const Layout& L, int NB,
+                                             int wave, int lane, EpiH<CTW, PTW>& er,
+                                             f16x8 (&w)[CTW][2]) {
     const WaveTilesH<F, CTW, PTW> wt(wave, lane);
     const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, NB));
     load_epi(er, prm + L.stem_b, isc, wt, lane);
     constexpr int CT = F / H2_TM;
     const f16x8* wf = reinterpret_cast<const f16x8*>(blob + h2_stem_off(F, NB)) + wt.ct0 * 64 + lane;
-    f16x8 w[CTW][2];
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
 #pragma unroll
         for (int p = 0; p < 2; ++p) w[c][p] = wf[(p * CT + c) * 64];
+}
+
+// the stem's operands are loaded up front (stem_h2_load, with the leaf planes): one global
+// round trip before the first MFMA instead of three dependent ones
+template <int F, int NBOARD, int CTW, int PTW>
+__device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__ out,
+                                        const f16x8 (&w)[CTW][2], int wave, int lane,
+                                        EpiH<CTW, PTW>& er, bool& ovf) {
+    const WaveTilesH<F, CTW, PTW> wt(wave, lane);
     const int kq = 8 * (lane >> 4);
     f16x8 a[PTW][2];
 #pragma unroll
@@ -1286,7 +1298,8 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         const int off = (t / 3 - 1) * 8 + (t % 3 - 1);
 #pragma unroll
         for (int u = 0; u < PTW; ++u) {
-            const int row = (pmask[u] >> t) & 1u ? wt.px[u] + off : C::ZROW;
+            const int nat = wt.px[u] + off;
+            const int row = (pmask[u] >> t) & 1u ? nat : C::ZROW + (nat & 7);
             const uint16_t* ap = in + C::at(row, 0, kq) + ks * C::KSP;
 #pragma unroll
             for (int p = 0; p < 2; ++p)
@@ -1321,14 +1334,42 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     epilogue_h2<F, NBOARD, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
 }
 
+// the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for
+// BS < 8, the unused rows/columns 0), staged through registers: the loads are issued with the
+// stem's weight loads, before anything waits
+template <int NBOARD, int BS, int NTHR>
+struct XinStage {
+    static constexpr int N = NBOARD * 100 * 4, PER = (N + NTHR - 1) / NTHR;
+    float v[PER];
+    __device__ void load(const float* __restrict__ x, int n_boards, int g0, int tid) {
+        constexpr int CELLS = BS * BS;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            const int i = tid + j * NTHR;
+            const int b = i / 400, rem = i % 400, p10 = rem >> 2, ch = rem & 3;
+            const int r = p10 / 10 - 1, c = p10 % 10 - 1, g = g0 + b;
+            const bool in = i < N && ch < 3 && (unsigned)r < (unsigned)BS &&
+                            (unsigned)c < (unsigned)BS && g < n_boards;
+            v[j] = in ? x[((size_t)g * 3 + ch) * CELLS + r * BS + c] : 0.0f;
+        }
+    }
+    __device__ void store(float* xin, int tid) const {
+#pragma unroll
+        for (int j = 0; j < PER; ++j)
+            if (tid + j * NTHR < N) xin[tid + j * NTHR] = v[j];
+    }
+};
+
 template <int F, int NBOARD, int CTW, int PTW, int BS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RVZ_H2_OCC, RVZ_H2_OCC)))
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
-                 float* __restrict__ work) {
+                 float* __restrict__ work, float* __restrict__ logits,
+                 float* __restrict__ value) {
     using C = CfgH<F, NBOARD>;
     using WT = WaveTilesH<F, CTW, PTW>;
     static_assert(WT::CG * (NBOARD * 64 / (PTW * H2_TN)) == 4, "4 waves");
+    static_assert((1024 + NBOARD * (192 + 256)) * 4 <= C::ACT * 2, "heads scratch fits in B");
     constexpr int NTHR = 256;
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
     uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
@@ -1340,8 +1381,8 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     bool ovf = false;
 
     // zero rows of both buffers, both parts, every k-step plane (4 * KS planes of KSP)
-    for (int i = tid; i < 4 * C::KS * H2_K; i += NTHR) {
-        const int plane = i / H2_K, k = i % H2_K;
+    for (int i = tid; i < 4 * C::KS * 8 * H2_K; i += NTHR) {
+        const int plane = i / (8 * H2_K), k = i % (8 * H2_K);
         actA[plane * C::KSP + C::ZROW * H2_K + k] = 0;
     }
     f16x8 bc[RVZ_H2_PD][CTW][2];
@@ -1354,10 +1395,14 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
 #pragma unroll
                 for (int p = 0; p < 2; ++p) bc[s][c][p] = wf[((s * 2 + p) * C::CT + c) * 64];
     }
-    load_input<NBOARD, BS>(x, n_boards, g0, xin, tid, NTHR);
-    __syncthreads();
+    XinStage<NBOARD, BS, NTHR> st;
+    st.load(x, n_boards, g0, tid);
     EpiH<CTW, PTW> er;
-    stem_h2<F, NBOARD, CTW, PTW>(xin, actA, blob, prm, L, n_blocks, wave, lane, er, ovf);
+    f16x8 ws[CTW][2];
+    stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+    st.store(xin, tid);
+    __syncthreads();
+    stem_h2<F, NBOARD, CTW, PTW>(xin, actA, ws, wave, lane, er, ovf);
     __syncthreads();
     const int64_t LW = h2_layer_elems(F);
     const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
@@ -1372,8 +1417,17 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                                                wave, lane, bc, er, ovf);
         __syncthreads();
     }
-    head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, reinterpret_cast<float*>(actB), prm, L,
-                                    HeadsGlobal{work, g0, n_boards}, tid);
+    if (logits) {          // the FC heads in this kernel: hpv and the fc1 output in buffer B
+        float* part = reinterpret_cast<float*>(actB);
+        float* hpv = part + 1024;
+        float* h1 = hpv + NBOARD * 192;
+        head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, part, prm, L, HeadsLds{hpv}, tid);
+        __syncthreads();
+        head_fcs<NBOARD, NTHR, BS>(hpv, h1, prm, L, g0, n_boards, logits, value, tid);
+    } else {
+        head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, reinterpret_cast<float*>(actB), prm,
+                                        L, HeadsGlobal{work, g0, n_boards}, tid);
+    }
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
 }
 
@@ -1443,16 +1497,16 @@ static void launch_trunk(const float* x, int32_t n, const float* params, const u
 
 template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
-                            int32_t filters, int32_t blocks, float* work, hipStream_t s) {
+                            int32_t filters, int32_t blocks, float* work, float* logits,
+                            float* value, hipStream_t s) {
     const Layout L = make_layout(filters, blocks, BS);
     if (filters == 64)
         hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, BS>), dim3((n + 1) / 2), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work);
+                           params, L, blob, blocks, work, logits, value);
     else
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, BS>), dim3(n), dim3(256), 0, s, x, n, params,
-                           L, blob, blocks, work);
+                           L, blob, blocks, work, logits, value);
 }
-
 
 extern "C" {
 
@@ -1596,8 +1650,8 @@ int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* p
     if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, s);
-    else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, s);
+    if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s);
+    else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
@@ -1605,6 +1659,20 @@ int rvz_resnet_fwd_h2(int32_t board, const float* x, int32_t n, const float* par
                       const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
                       float* logits, float* value, void* stream) {
     if (!logits || !value) return RVZ_EINVAL;
+#ifndef RVZ_H2_FC_IN
+#define RVZ_H2_FC_IN 0
+#endif
+    if (RVZ_H2_FC_IN) {     // one launch: the FC heads inside the trunk kernel
+        if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
+            (filters != 64 && filters != 128))
+            return RVZ_EINVAL;
+        if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
+        if (n == 0) return RVZ_OK;
+        hipStream_t s = (hipStream_t)stream;
+        if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, logits, value, s);
+        else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, logits, value, s);
+        return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+    }
     const int rc = rvz_resnet_trunk_h2(board, x, n, params, blob, filters, blocks, work, stream);
     if (rc != RVZ_OK) return rc;
     return rvz_resnet_heads_fc(board, work, n, params, filters, blocks, logits, value, stream);

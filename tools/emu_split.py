@@ -67,15 +67,21 @@ def forward(net, x, scheme, act_log2=0):
     x = x.double()
     r32 = (lambda t: t) if scheme == "exact64" else (lambda t: t.float().double())
     w, b = _fold(net.conv, net.bn)
-    h = F.relu(conv_scheme(x, w.double(), scheme, act_log2) + b.double().view(1, -1, 1, 1))
+    h = F.relu(conv_scheme(x, w.double(), scheme.replace("_lds", ""), act_log2)
+               + b.double().view(1, -1, 1, 1))
     h = r32(h)
     for blk in net.res_blocks:
         w1, b1 = _fold(blk.conv1, blk.bn1)
         w2, b2 = _fold(blk.conv2, blk.bn2)
-        y = F.relu(conv_scheme(h, w1.double(), scheme, act_log2) + b1.double().view(1, -1, 1, 1))
+        y = F.relu(conv_scheme(h, w1.double(), scheme.replace("_lds", ""), act_log2)
+                   + b1.double().view(1, -1, 1, 1))
         y = r32(y)
-        h = F.relu(conv_scheme(y, w2.double(), scheme, act_log2) + b2.double().view(1, -1, 1, 1)
-                   + h)
+        skip = h
+        if scheme.endswith("_lds"):   # skip input re-read as its two f16 parts (22 bits)
+            p0 = h.to(torch.float16).double()
+            skip = p0 + (h - p0).to(torch.float16).double()
+        h = F.relu(conv_scheme(y, w2.double(), scheme.replace("_lds", ""), act_log2)
+                   + b2.double().view(1, -1, 1, 1) + skip)
         h = r32(h)
     n = h.shape[0]
     wp, bp = _fold(net.policy_conv, net.policy_bn)
@@ -104,7 +110,7 @@ def main():
         l64, v64, h64 = forward(net, x, "exact64")
         scale = l64.abs().max().item()
         print(f"net {blocks}x{filters}, n={n}: logit scale {scale:.3g}, trunk max {h64.max():.3g}")
-        for s in ("fp32", "bf16x3_6", "f16x2_3", "f16x2_4", "f16x2_1acc"):
+        for s in ("fp32", "bf16x3_6", "f16x2_3", "f16x2_4", "f16x2_1acc", "f16x2_1acc_lds"):
             l, v, h = forward(net, x, s, act)
             print(f"{s:9s} max|dl|/scale {((l - l64).abs().max() / scale).item():.3e}  "
                   f"max|dv| {(v - v64).abs().max().item():.3e}  "

@@ -1,4 +1,6 @@
-"""Per-phase cycle split of the fused split-ResNet kernel (input+stem / trunk / heads).
+"""Per-phase cycle split of the fused ResNet trunk kernel (input+stem / trunk / heads).
+
+    KERNEL=h2|split python tools/phase_timing.py
 
 Builds a private copy of librvz with -DRVZ_PHASE_TIMING (s_memtime at phase boundaries, one
 record per workgroup), runs one forward at the bench batch and prints mean cycles per phase."""
@@ -29,19 +31,23 @@ out = {}
 for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
-    ev = rvz.LeafEvaluator(net, kernel="split")
+    kern = os.environ.get("KERNEL", "h2")
+    ev = rvz.LeafEvaluator(net, kernel=kern)
+    fwd = lib.rvz_resnet_fwd_h2 if kern == "h2" else lib.rvz_resnet_fwd_split
     x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
     lg = torch.empty(n, 65, device="cuda")
-    wk = torch.empty(n * 192, device="cuda")
+    wk = torch.zeros(n * 192 + 4, device="cuda")
     v = torch.empty(n, device="cuda")
     for _ in range(3):
-        rc = lib.rvz_resnet_fwd_split(8, C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
+        rc = fwd(8, C.c_void_p(x.data_ptr()), n, C.c_void_p(ev.params.data_ptr()),
                                       C.c_void_p(ev.wsplit.data_ptr()), filters, blocks,
                                       C.c_void_p(wk.data_ptr()), C.c_void_p(lg.data_ptr()), C.c_void_p(v.data_ptr()),
                                       C.c_void_p(_lib.stream_handle()))
         assert rc == 0
     torch.cuda.synchronize()
     nwg = (n + 1) // 2 if filters == 64 else n
+    if kern == "h2":     # persistent: one record per workgroup, phases of its first unit
+        nwg = min(nwg, 2 * torch.cuda.get_device_properties(0).multi_processor_count)
     buf = np.zeros((nwg, 8), np.uint64)
     assert lib.rvz_phase_read(buf.ctypes.data_as(C.c_void_p), nwg) == 0
     b = buf.astype(np.int64)
@@ -79,5 +85,11 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
     out[key]["wg_us_mean"] = float(wg_us.mean())
     out[key]["clock_ghz"] = float(tot.mean() / wg_us.mean() / 1e3)
     out[key]["kernel_span_us"] = float((rt[:, 1].max() - rt[:, 0].min()) / 100.0)
-    out[key]["busy_frac"] = float(wg_us.sum() / 256 / out[key]["kernel_span_us"])
+    occ = 2 if kern == "h2" else 1
+    out[key]["busy_frac"] = float(wg_us.sum() / (256 * occ) / out[key]["kernel_span_us"])
+    t0 = rt[:, 0].min()
+    st, en = (rt[:, 0] - t0) / 100.0, (rt[:, 1] - t0) / 100.0
+    out[key]["start_us_pct"] = [round(float(np.percentile(st, q)), 2) for q in (0, 10, 25, 50, 75, 90, 100)]
+    out[key]["end_us_pct"] = [round(float(np.percentile(en, q)), 2) for q in (0, 10, 25, 50, 75, 90, 100)]
+    out[key]["wg_us_pct"] = [round(float(np.percentile(wg_us, q)), 2) for q in (0, 10, 50, 90, 100)]
 print(json.dumps(out))

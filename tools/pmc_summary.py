@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"step": "k_step<", "act": "k_act<", "expand_backup": "k_expand_backup<",
-           "reset": "k_reset<", "nn_trunk": "k_resnet_split<", "nn_heads": "k_heads_fc(",
+           "reset": "k_reset<", "nn_trunk": ("k_resnet_h2<", "k_resnet_split<"), "nn_heads": "k_heads_fc(",
            "nn_conv3x3": "igemm_fwd_gtcx35_nhwc_fp32_bx0_ex1_bt128x64x16"}
 
 
@@ -29,7 +29,7 @@ def load(run_dir, counter):
             if r.get("Counter_Name") != counter:
                 continue
             for key, pat in KERNELS.items():
-                if pat in r["Kernel_Name"]:
+                if any(p in r["Kernel_Name"] for p in ((pat,) if isinstance(pat, str) else pat)):
                     per[key].append(float(r["Counter_Value"]))
     return per
 
