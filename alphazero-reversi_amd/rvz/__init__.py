@@ -7,6 +7,7 @@ Drop-in classes mirroring the reference's API (src/game, src/mcts, src/self_play
 Batched core:
     Engine                  n games + trees resident in HBM, C-ABI of include/rvz.h
     SelfPlayRunner          one ply per call, HIP-graph capturable
+    LaneRunner              independent lanes of SelfPlayRunners, one stream each, one graph
     AlphaZeroNetwork, LeafEvaluator   the policy/value net at the evaluation boundary
 """
 from ._lib import RvzError, load  # noqa: F401
@@ -14,6 +15,6 @@ from .engine import Engine, board_apply, board_canonical, board_legal  # noqa: F
 from .game import Board, ReversiGame  # noqa: F401
 from .mcts import MCTS  # noqa: F401
 from .network import AlphaZeroNetwork, LeafEvaluator, load_reference_state_dict  # noqa: F401
-from .selfplay import SelfPlay, SelfPlayRunner  # noqa: F401
+from .selfplay import LaneRunner, SelfPlay, SelfPlayRunner  # noqa: F401
 
 __version__ = "0.1.0"

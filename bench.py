@@ -65,6 +65,9 @@ def parse():
                          "auto choice), split (3-part bf16 split, 6 products), resnet (f32 MFMA), "
                          "miopen")
     ap.add_argument("--instrument-plies", type=int, default=2)
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="independent game lanes per GPU, one stream each in one graph "
+                         "(rvz.LaneRunner); the games are the same as with one lane")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
@@ -194,12 +197,29 @@ def main():
     nn_dtype = torch.float32 if args.nn_dtype == "fp32" else torch.bfloat16
 
     net = make_net(args, device)
-    ev = rvz.LeafEvaluator(net, dtype=nn_dtype, device=device, kernel=args.nn_kernel)
-    eng = rvz.Engine(args.games, args.sims, args.batch, 1.0, board_size=args.board, device=device,
-                     leaf_dtype=torch.float32 if nn_dtype == torch.float32 else torch.bfloat16)
+    leaf_dtype = torch.float32 if nn_dtype == torch.float32 else torch.bfloat16
+
+    def make_ev():
+        return rvz.LeafEvaluator(net, dtype=nn_dtype, device=device, kernel=args.nn_kernel)
+
+    def make_eng(n):
+        return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
+                          leaf_dtype=leaf_dtype)
+
     first_game = rank * args.games          # global game index space: rank r owns a shard
-    run = rvz.SelfPlayRunner(eng, ev, temperature=1.0, fused_softmax=True, autoreset=True,
+    if args.lanes > 1:
+        run = rvz.LaneRunner(make_eng, make_ev, args.games, args.lanes, temperature=1.0,
+                             fused_softmax=True, autoreset=True,
                              seed_base=args.seed + first_game, seed_stride=args.games * world)
+        lane0 = run.runners[0]
+        engines = [r.eng for r in run.runners]
+    else:
+        lane0 = run = rvz.SelfPlayRunner(make_eng(args.games), make_ev(), temperature=1.0,
+                                         fused_softmax=True, autoreset=True,
+                                         seed_base=args.seed + first_game,
+                                         seed_stride=args.games * world)
+        engines = [run.eng]
+    eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
     run.start()
 
     # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph
@@ -220,10 +240,11 @@ def main():
     t1 = time.perf_counter()
     rdist.barrier()
     s1 = int(run.steps.item())
-    eng.check()
+    for e in engines:
+        e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
 
-    ms, n, bytes_ = instrumented(run, eng, ev, args.instrument_plies)
+    ms, n, bytes_ = instrumented(lane0, eng, ev, args.instrument_plies)
     eng.check()
     kernels = {}
     for k in ("step", "act"):
@@ -234,18 +255,19 @@ def main():
     dom = max(("step", "act"),
               key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
     pmc = {}
-    if os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096:
+    if os.path.exists(args.pmc) and args.config == "c2" and eng.n_games == 4096:
         try:
             pmc = json.load(open(args.pmc))
         except Exception:
             pmc = {}
     traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
-    nn_flops = ev.flops_per_row() * args.games
+    lane_games = eng.n_games                # boards per NN launch
+    nn_flops = ev.flops_per_row() * lane_games
     nn_tflops = nn_flops / (ms["nn"] * 1e-3) / 1e12
     nn_per_ply = n["nn"] / max(1, args.instrument_plies)
     split = "nn_trunk" in ms
     if split:   # roofline of the NN trunk kernel: executed 16-bit MFMA FLOPs per launch / duration
-        mf = ev.mfma_flops_per_row() * args.games
+        mf = ev.mfma_flops_per_row() * lane_games
         nn_roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
                    "achieved": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12, 2),
                    "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
@@ -292,7 +314,8 @@ def main():
                        "nn_kernel": {"h2": "rvz_resnet_fwd_h2", "split": "rvz_resnet_fwd_split",
                                      "resnet": "rvz_resnet_fwd_f32"}
                        .get(getattr(ev, "kernel", ""), "miopen+rvz_nn_bias_act"),
-                       "graph": not args.no_graph, "parallelism": f"games sharded x{world}"},
+                       "graph": not args.no_graph, "lanes": args.lanes,
+                       "parallelism": f"games sharded x{world}"},
             # the dominant kernel of a ply (by time per ply) carries "roofline"; the other side
             # of the ply (NN vs search) is reported beside it
             "roofline": nn_roof if nn_dominant else search_roof,
