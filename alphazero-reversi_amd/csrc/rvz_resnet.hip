@@ -412,6 +412,105 @@ __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work
     }
 }
 
+// heads, part 2 on the f32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
+// accumulation — the arithmetic of an fp32 GEMM), 16 boards per workgroup: D = W X^T with rows =
+// output units (16-unit tiles: value fc1 16 tiles, policy fc ceil((cells+1)/16)), columns = the
+// 16 boards. The K order is permuted (step 4j + i uses k = 16j + 4g + i for lane group
+// g = lane >> 4), so a lane loads 4 consecutive k of its weight row (f32x4, L2) and of its
+// board's input row (ds_read_b128) per 4 MFMAs. Value fc2 (256 -> 1) + tanh reduce the fc1 tiles
+// through registers, lane shuffles and 64 floats of LDS.
+template <int BS>
+__global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ work, int n,
+                                                    const float* __restrict__ prm, Layout L,
+                                                    float* __restrict__ logits,
+                                                    float* __restrict__ value) {
+    constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
+    constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
+    constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
+    constexpr int VJ = VK / 16, PJ = PK / 16, VTW = 256 / 16 / 4, PTW = (PT + 3) / 4;
+    static_assert(CELLS % 4 == 0 && PIN % 4 == 0, "f32x4 rows");
+    __shared__ __attribute__((aligned(16))) float in[16 * ROW];
+    __shared__ float vpart[4][16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g0 = blockIdx.x * 16, col = lane & 15, grp = lane >> 4;
+    // every weight fragment of this wave's tiles, issued before anything waits: value fc1 tiles
+    // wave + 4m, policy tiles wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
+    f32x4 av[VTW][VJ], ap[PTW][PJ];
+#pragma unroll
+    for (int m = 0; m < VTW; ++m) {
+        const float* wr = prm + L.vfc1_w + (size_t)(16 * (wave + 4 * m) + col) * CELLS + 4 * grp;
+#pragma unroll
+        for (int j = 0; j < VJ; ++j)
+            av[m][j] = 16 * j + 4 * grp < CELLS ? *reinterpret_cast<const f32x4*>(wr + 16 * j)
+                                                : f32x4{};
+    }
+#pragma unroll
+    for (int m = 0; m < PTW; ++m) {
+        const int o = 16 * (wave + 4 * m) + col;
+        const float* wr = prm + L.pfc_w + (size_t)o * PIN + 4 * grp;
+#pragma unroll
+        for (int j = 0; j < PJ; ++j)
+            ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
+                           ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
+    }
+    for (int i = tid; i < 16 * (PK + VK); i += 256) {
+        const int b = i / (PK + VK), k = i % (PK + VK), g = g0 + b;
+        float v = 0.0f;
+        if (g < n) {
+            if (k < PIN) v = work[(size_t)g * 192 + k];
+            else if (k >= PK && k - PK < CELLS) v = work[(size_t)g * 192 + PIN + (k - PK)];
+        }
+        in[b * ROW + k] = v;
+    }
+    __syncthreads();
+    const float* inb = in + col * ROW + 4 * grp;
+    // value fc1 (+ bias, ReLU) and its fc2 partial
+    float vp = 0.0f;
+#pragma unroll
+    for (int m = 0; m < VTW; ++m) {
+        f32x4 acc = {};
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + PK + 16 * j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][j][i], bx[i], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {                // D row = unit 16t + 4grp + r, col = board
+            const int uu = 16 * (wave + 4 * m) + 4 * grp + r;
+            vp = fmaf(fmaxf(acc[r] + prm[L.vfc1_b + uu], 0.0f), prm[L.vfc2_w + uu], vp);
+        }
+    }
+    vp += __shfl_xor(vp, 16);
+    vp += __shfl_xor(vp, 32);
+    if (grp == 0) vpart[wave][col] = vp;
+    // policy fc
+#pragma unroll
+    for (int m = 0; m < PTW; ++m) {
+        const int t = wave + 4 * m;
+        if (t >= PT) break;
+        f32x4 acc = {};
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + 16 * j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[m][j][i], bx[i], acc, 0, 0, 0);
+        }
+        const int g = g0 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int oo = 16 * t + 4 * grp + r;
+            if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
+        }
+    }
+    __syncthreads();
+    if (tid < 16 && g0 + tid < n)
+        value[g0 + tid] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
+                                prm[L.vfc2_b]);
+}
+
 // =============================================================================================
 // f32 MFMA kernel
 
@@ -546,11 +645,22 @@ __device__ uint64_t g_wave[65536][16];
     if (threadIdx.x == 0 && blockIdx.x < 65536) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
 #define RT(i) \
     if (threadIdx.x == 0 && blockIdx.x < 65536) g_rt[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
+__device__ uint64_t g_stem[65536][8];
+__device__ uint32_t g_hwid[65536][2];   // HW_ID (CU, SE, ...), XCC_ID of each workgroup
+#define HWID() \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) { \
+        g_hwid[blockIdx.x][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4); \
+        g_hwid[blockIdx.x][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
+    }
+#define STEM_T(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_stem[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
 #define WAVE_T(i) \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 65536) \
         g_wave[blockIdx.x][(threadIdx.x >> 6) + 8 * (i)] = __builtin_amdgcn_s_memtime()
 #else
 #define PHASE(i)
+#define HWID()
+#define STEM_T(i)
 #define WAVE_T(i)
 #define RT(i)
 #endif
@@ -1096,7 +1206,7 @@ struct CfgH {
     static constexpr int CT = F / H2_TM;
     static_assert(XIN * 4 <= ACT * 2, "xin fits in buffer B");
     static_assert((PLANE * 2) % 16 == 0 && (KSP * 2) % 16 == 0, "16-byte aligned planes");
-    static_assert(BYTES * RVZ_H2_OCC <= 160 * 1024, "LDS for RVZ_H2_OCC workgroups per CU");
+    static_assert(BYTES * RVZ_H2_OCC <= 160 * 1024 || NBOARD == 1, "LDS for the occupancy");
     // halves offset of (row, k-step plane ks, 8-channel slot q in 0..3)
     static __device__ __forceinline__ int at(int row, int ks, int q) {
         return ks * KSP + row * H2_K + 8 * (q ^ ((row >> 1) & 3));
@@ -1129,10 +1239,16 @@ struct WaveTilesH {
     }
 };
 
+// RVZ_H2_SKIP_LDS 1: the skip input is re-read from LDS as its two parts (x0 + x1, 22 bits) at
+// the place conv B overwrites, instead of kept in 32 fp32 registers (frees them for a deeper
+// weight prefetch; no measurable error change, tools/emu_split.py f16x2_1acc_lds)
+#ifndef RVZ_H2_SKIP_LDS
+#define RVZ_H2_SKIP_LDS 0
+#endif
 template <int CTW, int PTW>
 struct EpiH {
     f32x4 bias[CTW], isc[CTW];       // per out-channel bias, inverse weight scale
-    float res[CTW][PTW][4];          // the block input (fp32) of this lane's outputs
+    float res[CTW][PTW][RVZ_H2_SKIP_LDS ? 1 : 4];   // the block input (fp32) of this lane's outputs
 };
 
 template <int F, int CTW, int PTW>
@@ -1156,12 +1272,18 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                                             bool& ovf) {
     using C = CfgH<F, NBOARD>;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
 #pragma unroll
         for (int u = 0; u < PTW; ++u) {
             const int n0 = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
             const int o = C::at(wt.px[u], n0 / H2_K, (n0 % H2_K) >> 3) + (n0 & 4);
+            f16x4 s0, s1;
+            if (RES && RVZ_H2_SKIP_LDS) {
+                s0 = *reinterpret_cast<const f16x4*>(out + o);
+                s1 = *reinterpret_cast<const f16x4*>(out + C::PLANE + o);
+            }
             u32x2 d0, d1;
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
@@ -1170,10 +1292,13 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                 for (int e = 0; e < 2; ++e) {
                     const int j = 2 * hf + e;
                     float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]);
-                    if (RES) x += er.res[c][u][j];
+                    if (RES) {
+                        if constexpr (RVZ_H2_SKIP_LDS) x += (float)s0[j] + (float)s1[j];
+                        else x += er.res[c][u][j];
+                    }
                     x = fmaxf(x, 0.0f);
                     ovf |= x >= 65520.0f;
-                    if (KEEP) er.res[c][u][j] = x;
+                    if constexpr (KEEP && !RVZ_H2_SKIP_LDS) er.res[c][u][j] = x;
                     v[e] = x;
                 }
                 uint32_t h0, h1;
@@ -1254,7 +1379,16 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
     for (int c = 0; c < CTW; ++c)
 #pragma unroll
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
+    STEM_T(4);
     mma3(acc, a, w);
+    {   // wait for the MFMAs (stamp only)
+#ifdef RVZ_PHASE_TIMING
+        float z = acc[0][0][0];
+        asm volatile("" : "+v"(z));
+        if (z == 12345.678f) STEM_T(6);
+#endif
+    }
+    STEM_T(5);
     epilogue_h2<F, NBOARD, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
 }
 
@@ -1360,8 +1494,8 @@ struct XinStage {
     }
 };
 
-template <int F, int NBOARD, int CTW, int PTW, int BS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RVZ_H2_OCC, RVZ_H2_OCC)))
+template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, float* __restrict__ logits,
@@ -1379,6 +1513,9 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = blockIdx.x * NBOARD;
     bool ovf = false;
+    PHASE(0);
+    RT(0);
+    HWID();
 
     // zero rows of both buffers, both parts, every k-step plane (4 * KS planes of KSP)
     for (int i = tid; i < 4 * C::KS * 8 * H2_K; i += NTHR) {
@@ -1400,10 +1537,15 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     EpiH<CTW, PTW> er;
     f16x8 ws[CTW][2];
     stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+    STEM_T(0);
     st.store(xin, tid);
+    STEM_T(1);
     __syncthreads();
+    STEM_T(2);
     stem_h2<F, NBOARD, CTW, PTW>(xin, actA, ws, wave, lane, er, ovf);
+    STEM_T(3);
     __syncthreads();
+    PHASE(1);
     const int64_t LW = h2_layer_elems(F);
     const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
     for (int blk = 0; blk < n_blocks; ++blk) {
@@ -1411,12 +1553,15 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         conv_h2<F, NBOARD, CTW, PTW, false, BS>(actA, actB, blob + l1 * LW,
                                                 prm + L.res_b + (size_t)l1 * F, isc + l1 * F,
                                                 wave, lane, bc, er, ovf);
+        if (blk == 0) PHASE(5);
         __syncthreads();
+        if (blk == 0) PHASE(6);
         conv_h2<F, NBOARD, CTW, PTW, true, BS>(actB, actA, blob + l2 * LW,
                                                prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
                                                wave, lane, bc, er, ovf);
         __syncthreads();
     }
+    PHASE(2);
     if (logits) {          // the FC heads in this kernel: hpv and the fc1 output in buffer B
         float* part = reinterpret_cast<float*>(actB);
         float* hpv = part + 1024;
@@ -1428,6 +1573,8 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, reinterpret_cast<float*>(actB), prm,
                                         L, HeadsGlobal{work, g0, n_boards}, tid);
     }
+    PHASE(3);
+    RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
 }
 
@@ -1495,16 +1642,27 @@ static void launch_trunk(const float* x, int32_t n, const float* params, const u
                            dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
 }
 
+// F = 64: RVZ_H2_NB64 boards per workgroup — 2 (2 x 4 tiles per wave, 2 workgroups per CU) or
+// 1 (2 x 2 tiles per wave, 4 workgroups per CU)
+#ifndef RVZ_H2_NB64
+#define RVZ_H2_NB64 2
+#endif
 template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
                             int32_t filters, int32_t blocks, float* work, float* logits,
                             float* value, hipStream_t s) {
     const Layout L = make_layout(filters, blocks, BS);
-    if (filters == 64)
-        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, BS>), dim3((n + 1) / 2), dim3(256), 0, s, x, n,
+#ifndef RVZ_H2_DYN_LDS
+#define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
+#endif
+    if (filters == 64 && RVZ_H2_NB64 == 2)
+        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, BS, 2>), dim3((n + 1) / 2), dim3(256),
+                           RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value);
+    else if (filters == 64)
+        hipLaunchKernelGGL((k_resnet_h2<64, 1, 2, 2, BS, 4>), dim3(n), dim3(256), 0, s, x, n,
                            params, L, blob, blocks, work, logits, value);
     else
-        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, BS>), dim3(n), dim3(256), 0, s, x, n, params,
+        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, BS, 2>), dim3(n), dim3(256), 0, s, x, n, params,
                            L, blob, blocks, work, logits, value);
 }
 
@@ -1541,6 +1699,14 @@ int rvz_resnet_fwd_f32(int32_t board, const float* x, int32_t n, const float* pa
 }
 
 #ifdef RVZ_PHASE_TIMING
+int rvz_hwid_read(uint32_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hwid), (size_t)n * 2 * sizeof(uint32_t)) ==
+                   hipSuccess ? 0 : -5;
+}
+int rvz_stem_read(uint64_t* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stem), (size_t)n * 8 * sizeof(uint64_t)) ==
+                   hipSuccess ? 0 : -5;
+}
 int rvz_rt_read(uint64_t* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rt), (size_t)n * 2 * sizeof(uint64_t)) ==
                    hipSuccess ? 0 : -5;
@@ -1601,6 +1767,19 @@ int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float
     if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     const Layout L = make_layout(filters, blocks, board);
+#ifndef RVZ_HEADS_MFMA
+#define RVZ_HEADS_MFMA 1
+#endif
+    if (RVZ_HEADS_MFMA) {
+        const dim3 grid((n + 15) / 16), block(256);
+        if (board == 8)
+            hipLaunchKernelGGL(k_heads_mfma<8>, grid, block, 0, (hipStream_t)stream, work, n,
+                               params, L, logits, value);
+        else
+            hipLaunchKernelGGL(k_heads_mfma<6>, grid, block, 0, (hipStream_t)stream, work, n,
+                               params, L, logits, value);
+        return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+    }
     const dim3 grid((n + FCB - 1) / FCB), block(256);
     if (board == 8)
         hipLaunchKernelGGL(k_heads_fc<8>, grid, block, 0, (hipStream_t)stream, work, n, params,

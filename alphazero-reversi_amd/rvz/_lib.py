@@ -15,7 +15,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librvz.so")
+LIB_PATH = os.environ.get("RVZ_LIB", os.path.join(_HERE, "librvz.so"))   # RVZ_LIB: experiments
 
 RVZ_OK, RVZ_DONE = 0, 1
 RVZ_LEAF_F32, RVZ_LEAF_BF16 = 0, 1

@@ -31,6 +31,10 @@ def conv_scheme(x, w, scheme, act_log2):
     """x [n,c,8,8] fp64 holding fp32 values, w [o,c,3,3] fp64 holding fp32 values."""
     if scheme == "exact64":
         return F.conv2d(x, w, padding=1)
+    if scheme == "wino32":
+        return winograd(x, w, False)
+    if scheme == "wino_h2":
+        return winograd(x, w, True)
     if scheme == "fp32":
         return F.conv2d(x.float(), w.float(), padding=1).double()
     if scheme == "bf16x3_6":
@@ -59,6 +63,39 @@ def conv_scheme(x, w, scheme, act_log2):
         lo = lo + conv(xs[i], ws[j])
     y = (hi + lo).double()
     return y / (sx * sw.view(1, -1, 1, 1))
+
+
+BT = torch.tensor([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], dtype=torch.float64)
+G = torch.tensor([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], dtype=torch.float64)
+AT = torch.tensor([[1, 1, 1, 0], [0, 1, -1, -1]], dtype=torch.float64)
+
+
+def winograd(x, w, f16split, acc32=True):
+    """F(2x2, 3x3) Winograd conv (pad 1) on 8x8 boards: input / output transforms in fp32, weights
+    transformed in fp64 then rounded to fp32, the 16 per-position GEMMs with the operands split
+    into two f16 parts (3 products, weights scaled per out-channel) or in fp32."""
+    n, c = x.shape[:2]
+    o = w.shape[0]
+    xp = F.pad(x.float(), (1, 1, 1, 1))                       # [n,c,10,10] fp32
+    # tiles: output (ty,tx) in 4x4, input patch padded rows 2ty..2ty+3
+    d = xp.unfold(2, 4, 2).unfold(3, 4, 2)                    # [n,c,4,4,4,4] (ty,tx,i,j)
+    bt = BT.float()
+    v = torch.einsum("ai,nctxij,bj->nctxab", bt, d, bt)       # fp32 transforms
+    u = torch.einsum("ai,ocij,bj->ocab", G, w.double(), G).float()   # [o,c,4,4]
+    if f16split:
+        m = u.double().abs().amax(dim=(1, 2, 3)).clamp_min(1e-30)
+        sw = torch.exp2(14 - torch.floor(torch.log2(m)))
+        us = parts(u.double() * sw.view(-1, 1, 1, 1), torch.float16, 2)
+        vs = parts(v.double(), torch.float16, 2)
+        prod = lambda a, b: torch.einsum("ocab,nctxab->notxab", a.float(), b.float())  # noqa
+        mm = (prod(us[0], vs[0]) + prod(us[1], vs[0]) + prod(us[0], vs[1])).double()
+        mm = mm / sw.view(1, -1, 1, 1, 1, 1)
+        mm = mm.float()
+    else:
+        mm = torch.einsum("ocab,nctxab->notxab", u, v)         # fp32
+    at = AT.float()
+    y = torch.einsum("pa,notxab,qb->notxpq", at, mm, at)      # [n,o,4,4,2,2] fp32
+    return y.permute(0, 1, 2, 4, 3, 5).reshape(n, o, 8, 8).double()
 
 
 def forward(net, x, scheme, act_log2=0):
@@ -110,7 +147,7 @@ def main():
         l64, v64, h64 = forward(net, x, "exact64")
         scale = l64.abs().max().item()
         print(f"net {blocks}x{filters}, n={n}: logit scale {scale:.3g}, trunk max {h64.max():.3g}")
-        for s in ("fp32", "bf16x3_6", "f16x2_3", "f16x2_4", "f16x2_1acc", "f16x2_1acc_lds"):
+        for s in ("fp32", "f16x2_1acc", "wino32", "wino_h2"):
             l, v, h = forward(net, x, s, act)
             print(f"{s:9s} max|dl|/scale {((l - l64).abs().max() / scale).item():.3e}  "
                   f"max|dv| {(v - v64).abs().max().item():.3e}  "

@@ -46,38 +46,33 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
         assert rc == 0
     torch.cuda.synchronize()
     nwg = (n + 1) // 2 if filters == 64 else n
-    if kern == "h2":     # persistent: one record per workgroup, phases of its first unit
-        nwg = min(nwg, 2 * torch.cuda.get_device_properties(0).multi_processor_count)
     buf = np.zeros((nwg, 8), np.uint64)
     assert lib.rvz_phase_read(buf.ctypes.data_as(C.c_void_p), nwg) == 0
     b = buf.astype(np.int64)
     wv = np.zeros((nwg, 16), np.uint64)
     assert lib.rvz_wave_read(wv.ctypes.data_as(C.c_void_p), nwg) == 0
     wv = wv.astype(np.int64)
-    kl = wv[:, :8] - b[:, 1:2]          # per wave: k-loop end of layer 0, from the layer start
-    ep = wv[:, 8:] - b[:, 1:2]          # per wave: epilogue end
-    out[f"{blocks}x{filters}_waves"] = {"kloop_end": [round(float(v)) for v in kl.mean(0)],
-                                        "epi_end": [round(float(v)) for v in ep.mean(0)],
-                                        "kloop_end_max_mean": float(kl.max(1).mean())}
     d = np.diff(b[:, :4], axis=1)
     tot = b[:, 3] - b[:, 0]
     key = f"{blocks}x{filters}"
     out[key] = {"stem": float(d[:, 0].mean()), "trunk": float(d[:, 1].mean()),
                 "per_layer": float(d[:, 1].mean() / (2 * blocks)), "heads": float(d[:, 2].mean()),
                 "wg_total": float(tot.mean()),
-                "l0_kloop": float((b[:, 4] - b[:, 1]).mean()),
-                "l0_epilogue": float((b[:, 5] - b[:, 4]).mean()),
+                "l0_conv_a": float((b[:, 5] - b[:, 1]).mean()),
                 "l0_barrier": float((b[:, 6] - b[:, 5]).mean()),
                 "n_wg": nwg}
     if hasattr(lib, "rvz_stem_read"):    # builds with the stem stamps (STEM_T)
-        st = np.zeros((nwg, 4), np.uint64)
+        st = np.zeros((nwg, 8), np.uint64)
         assert lib.rvz_stem_read(st.ctypes.data_as(C.c_void_p), nwg) == 0
         st = st.astype(np.int64)
-        out[key]["stem_split"] = {"loads_zero": float((st[:, 0] - b[:, 0]).mean()),
-                                  "sync1": float((st[:, 1] - st[:, 0]).mean()),
-                                  "xin_write_sync2": float((st[:, 2] - st[:, 1]).mean()),
+        out[key]["stem_split"] = {"zero_rows_issue_loads": float((st[:, 0] - b[:, 0]).mean()),
+                                  "xin_store_wait_loads": float((st[:, 1] - st[:, 0]).mean()),
+                                  "sync1": float((st[:, 2] - st[:, 1]).mean()),
                                   "stem_compute": float((st[:, 3] - st[:, 2]).mean()),
-                                  "sync3": float((b[:, 1] - st[:, 3]).mean())}
+                                  "im2col_split": float((st[:, 4] - st[:, 2]).mean()),
+                                  "mfma": float((st[:, 5] - st[:, 4]).mean()),
+                                  "epilogue": float((st[:, 3] - st[:, 5]).mean()),
+                                  "sync2": float((b[:, 1] - st[:, 3]).mean())}
     rt = np.zeros((nwg, 2), np.uint64)
     assert lib.rvz_rt_read(rt.ctypes.data_as(C.c_void_p), nwg) == 0
     rt = rt.astype(np.int64)
@@ -85,11 +80,38 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
     out[key]["wg_us_mean"] = float(wg_us.mean())
     out[key]["clock_ghz"] = float(tot.mean() / wg_us.mean() / 1e3)
     out[key]["kernel_span_us"] = float((rt[:, 1].max() - rt[:, 0].min()) / 100.0)
-    occ = 2 if kern == "h2" else 1
+    occ = int(os.environ.get("OCC", 2 if kern == "h2" else 1))
     out[key]["busy_frac"] = float(wg_us.sum() / (256 * occ) / out[key]["kernel_span_us"])
     t0 = rt[:, 0].min()
     st, en = (rt[:, 0] - t0) / 100.0, (rt[:, 1] - t0) / 100.0
     out[key]["start_us_pct"] = [round(float(np.percentile(st, q)), 2) for q in (0, 10, 25, 50, 75, 90, 100)]
     out[key]["end_us_pct"] = [round(float(np.percentile(en, q)), 2) for q in (0, 10, 25, 50, 75, 90, 100)]
     out[key]["wg_us_pct"] = [round(float(np.percentile(wg_us, q)), 2) for q in (0, 10, 50, 90, 100)]
+    if hasattr(lib, "rvz_hwid_read") and kern == "h2":
+        hw = np.zeros((nwg, 2), np.uint32)
+        assert lib.rvz_hwid_read(hw.ctypes.data_as(C.c_void_p), nwg) == 0
+        # CU identity: XCC, SE (bits 13-15), SH (12), CU (8-11)
+        cu = (hw[:, 1].astype(np.int64) & 0xF) * 4096 + ((hw[:, 0] >> 8) & 0xFF).astype(np.int64)
+        by = {}
+        for w in range(nwg):
+            by.setdefault(int(cu[w]), []).append(w)
+        # per CU: workgroups in dispatch order; partner pairs = those resident at the same time
+        st0, en0 = rt[:, 0], rt[:, 1]
+        dstart, pairs, first_pair = [], 0, []
+        for c, ws in by.items():
+            ws.sort(key=lambda w: st0[w])
+            for i, w in enumerate(ws):
+                for v in ws[i + 1:]:
+                    if st0[v] < en0[w]:            # overlapping lifetimes: co-resident
+                        dstart.append(abs(int(st0[v]) - int(st0[w])) / 100.0)
+                        pairs += 1
+                        if len(first_pair) < 8:
+                            first_pair.append([w, v])
+        d = np.array(dstart) if dstart else np.zeros(1)
+        out[key]["cus_used"] = len(by)
+        out[key]["wg_per_cu"] = [min(len(v) for v in by.values()), max(len(v) for v in by.values())]
+        out[key]["coresident_pairs"] = pairs
+        out[key]["pair_start_gap_us_pct"] = [round(float(np.percentile(d, q)), 2)
+                                             for q in (10, 25, 50, 75, 90)]
+        out[key]["example_pairs"] = first_pair
 print(json.dumps(out))
