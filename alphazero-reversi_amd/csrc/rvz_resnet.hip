@@ -666,8 +666,8 @@ __device__ uint32_t g_hwid[65536][2];   // HW_ID (CU, SE, ...), XCC_ID of each w
 #endif
 
 // MFMA shape traits (D = W X^T: TM output channels x TN pixels, K input channels per step)
-struct Shape32 {   // v_mfma_f32_32x32x16_bf16
-    static constexpr int TM = 32, TN = 32, K = 16, NG = 4;
+struct Shape32 {   // v_mfma_f32_32x32x16_bf16 (RVZ_SPLIT_SHAPE=32)
+    [[maybe_unused]] static constexpr int TM = 32, TN = 32, K = 16, NG = 4;
     typedef f32x16 acc_t;
     // channel offset (within the tile) of register group g; registers 4g .. 4g+3
     static __device__ __forceinline__ int chan(int g, int lane) { return 8 * g + 4 * (lane >> 5); }
