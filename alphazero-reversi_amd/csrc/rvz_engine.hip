@@ -254,6 +254,24 @@ __device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lan
     return root_n;
 }
 
+// rvz_search_skip: the last batch's leaf is not evaluated. Its evaluation would only set the
+// leaf's children priors and add the value to W along the path — state the discarded tree never
+// reads again — while the visit counts grow by the queued copies regardless (mcts.py:625-640), so
+// N alone is backed up here and the visits, p and the move are those of the evaluated search.
+__device__ __forceinline__ void backup_visits_only(const View& v, int g, int lane,
+                                                   unsigned long long& ab) {
+    const int copies = v.pend[g], plen = v.plen[g];
+    if (copies == 0) return;
+    const int path_reg = lane < plen ? v.path[g * PATH_CAP + lane] : 0;
+    Node* nodes = v.nodes + (size_t)g * v.M;
+    const int j = plen - 1 - lane;
+    const int nid = __shfl(path_reg, j < 0 ? 0 : j);
+    if (lane < plen) nodes[nid].n += copies;
+    if (lane == 0) v.pend[g] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    if (v.stats) ab += 8ull + 4ull * plen + 8ull * plen;
+}
+
 // select: mcts.py:348-386 for one batch of `bsz` traversals + _process_batch pass 1 (:561-585).
 // root / root_meta / root_n were loaded (or produced by the expand phase) by the caller.
 template <int BS, typename XT>
@@ -401,15 +419,20 @@ __global__ __launch_bounds__(256) void k_step(View v, int expand, const float* _
 }
 
 template <int BS>
-__global__ __launch_bounds__(256) void k_expand_backup(View v, const float* __restrict__ policy,
+__global__ __launch_bounds__(256) void k_expand_backup(View v, int mode,
+                                                       const float* __restrict__ policy,
                                                        int is_logits,
                                                        const float* __restrict__ value) {
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (g >= v.G) return;
     unsigned long long ab = 0;
-    const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
-    expand_backup_phase<BS>(v, g, lane, x, is_logits, nullptr, ab);
+    if (mode == 2) {
+        backup_visits_only(v, g, lane, ab);
+    } else {
+        const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
+        expand_backup_phase<BS>(v, g, lane, x, is_logits, nullptr, ab);
+    }
     if (v.stats && lane == 0) v.stats[2 * (size_t)v.G + g] += ab;
 }
 
@@ -464,9 +487,11 @@ __global__ __launch_bounds__(256) void k_act(View v, int expand, const float* __
     const int g = blockIdx.x * WPB + wid;
     if (g >= v.G) return;
     unsigned long long ab = 0;
-    if (expand) {
+    if (expand == 1) {
         const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
         expand_backup_phase<BS>(v, g, lane, x, is_logits, nullptr, ab);
+    } else if (expand == 2) {
+        backup_visits_only(v, g, lane, ab);
     }
     GameS gm = load_game(v, g);
     double* prow = out_p + (size_t)g * NPOL;
@@ -992,8 +1017,8 @@ int rvz_search_submit(rvz_engine* e, const float* policy, int32_t is_logits, con
 static int flush_pending(rvz_engine* e) {
     if (!e->pending) return RVZ_OK;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
-    if (e->BS == 8) hipLaunchKernelGGL(k_expand_backup<8>, grid, block, 0, e->stream, e->v, e->pend_policy, e->pend_is_logits, e->pend_value);
-    else hipLaunchKernelGGL(k_expand_backup<6>, grid, block, 0, e->stream, e->v, e->pend_policy, e->pend_is_logits, e->pend_value);
+    if (e->BS == 8) hipLaunchKernelGGL(k_expand_backup<8>, grid, block, 0, e->stream, e->v, e->pending, e->pend_policy, e->pend_is_logits, e->pend_value);
+    else hipLaunchKernelGGL(k_expand_backup<6>, grid, block, 0, e->stream, e->v, e->pending, e->pend_policy, e->pend_is_logits, e->pend_value);
     e->pending = 0;
     return launch_check(e, "k_expand_backup");
 }
@@ -1006,6 +1031,18 @@ int rvz_search_visits(rvz_engine* e, int32_t* out) {
     if (e->BS == 8) hipLaunchKernelGGL(k_visits<8>, grid, block, 0, e->stream, e->v, out);
     else hipLaunchKernelGGL(k_visits<6>, grid, block, 0, e->stream, e->v, out);
     return launch_check(e, "k_visits");
+}
+
+int rvz_search_skip(rvz_engine* e) {
+    if (!e) return RVZ_EINVAL;
+    const int S = e->cfg.num_simulations, B = e->cfg.batch_size;
+    if (!e->searching || e->next_batch == 0 || e->next_batch * B < S) {
+        e->err = "rvz_search_skip is only valid after the last rvz_search_step of a search";
+        return RVZ_EINVAL;
+    }
+    if (e->pending) { e->err = "rvz_search_skip after rvz_search_submit"; return RVZ_EINVAL; }
+    e->pending = 2;   // rvz_act: visit counts only
+    return RVZ_OK;
 }
 
 int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, int32_t* out_idx,

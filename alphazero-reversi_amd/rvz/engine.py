@@ -202,14 +202,25 @@ class Engine:
         # the expand + backup is deferred into the next launch: keep the rows alive until then
         self._keep = (policy, value)
 
+    def search_skip(self):
+        """Leave the last batch unevaluated (rvz_search_skip): same visits, p and move."""
+        self._stream()
+        self._call("rvz_search_skip")
+
     def search(self, evaluator: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],
-               fused_softmax: bool = True):
+               fused_softmax: bool = True, skip_last_eval: bool = False):
         """MCTS.search for every live game. evaluator(leaf_x) -> (logits, value).
 
         fused_softmax=False applies torch's F.softmax (the reference's mcts.py:596) before the
-        expand kernel instead of the kernel's fused softmax."""
+        expand kernel instead of the kernel's fused softmax. skip_last_eval=True does not
+        evaluate the last batch (rvz_search_skip; bit-identical visits, one NN call fewer)."""
         self.search_begin()
+        k = 0
         while self.search_step():
+            k += 1
+            if skip_last_eval and k == self.n_batches:
+                self.search_skip()
+                break
             logits, value = evaluator(self.leaf_x)
             logits = logits.float().contiguous()
             value = value.float().contiguous()

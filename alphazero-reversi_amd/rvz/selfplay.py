@@ -27,8 +27,10 @@ from .engine import Engine, board_canonical
 class SelfPlayRunner:
     def __init__(self, engine: Engine, evaluator: Callable, temperature: float = 1.0,
                  fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
-                 record: bool = False, max_plies: int = 60, seed_stride: int = None):
+                 record: bool = False, max_plies: int = 60, seed_stride: int = None,
+                 skip_last_eval: bool = False):
         self.eng = engine
+        self.skip_last_eval = bool(skip_last_eval)
         self.evaluator = evaluator
         self.temperature = float(temperature)
         self.fused_softmax = fused_softmax
@@ -67,7 +69,8 @@ class SelfPlayRunner:
         self.pre_black.copy_(b)
         self.pre_white.copy_(w)
         self.pre_status.copy_(st)
-        eng.search(self.evaluator, fused_softmax=self.fused_softmax)
+        eng.search(self.evaluator, fused_softmax=self.fused_softmax,
+                   skip_last_eval=self.skip_last_eval)
         idx, _ = eng.act(self.temperature, apply=True)
         self.steps += (idx >= 0).sum()
         _, _, st = eng.get_state()
@@ -123,14 +126,15 @@ class LaneRunner:
     def __init__(self, make_engine: Callable[[int], Engine], make_evaluator: Callable,
                  n_games: int, lanes: int = 2, temperature: float = 1.0,
                  fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
-                 seed_stride: int = None):
+                 seed_stride: int = None, skip_last_eval: bool = False):
         if lanes < 1 or n_games % lanes:
             raise ValueError("n_games must be a multiple of lanes")
         gl = n_games // lanes
         stride = n_games if seed_stride is None else int(seed_stride)
         self.runners = [SelfPlayRunner(make_engine(gl), make_evaluator(), temperature,
                                        fused_softmax, autoreset, seed_base + k * gl,
-                                       seed_stride=stride) for k in range(lanes)]
+                                       seed_stride=stride, skip_last_eval=skip_last_eval)
+                        for k in range(lanes)]
         dev = self.runners[0].eng.device
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)]
         self.temperature = float(temperature)

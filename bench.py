@@ -65,6 +65,9 @@ def parse():
                          "auto choice), split (3-part bf16 split, 6 products), resnet (f32 MFMA), "
                          "miopen")
     ap.add_argument("--instrument-plies", type=int, default=2)
+    ap.add_argument("--skip-last-eval", action="store_true",
+                    help="leave each search's last batch unevaluated (rvz_search_skip): "
+                         "bit-identical games, one NN call fewer per move; off for the headline")
     ap.add_argument("--lanes", type=int, default=1,
                     help="independent game lanes per GPU, one stream each in one graph "
                          "(rvz.LaneRunner); the games are the same as with one lane")
@@ -210,14 +213,16 @@ def main():
     if args.lanes > 1:
         run = rvz.LaneRunner(make_eng, make_ev, args.games, args.lanes, temperature=1.0,
                              fused_softmax=True, autoreset=True,
-                             seed_base=args.seed + first_game, seed_stride=args.games * world)
+                             seed_base=args.seed + first_game, seed_stride=args.games * world,
+                             skip_last_eval=args.skip_last_eval)
         lane0 = run.runners[0]
         engines = [r.eng for r in run.runners]
     else:
         lane0 = run = rvz.SelfPlayRunner(make_eng(args.games), make_ev(), temperature=1.0,
                                          fused_softmax=True, autoreset=True,
                                          seed_base=args.seed + first_game,
-                                         seed_stride=args.games * world)
+                                         seed_stride=args.games * world,
+                                         skip_last_eval=args.skip_last_eval)
         engines = [run.eng]
     eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
     run.start()
@@ -315,6 +320,7 @@ def main():
                                      "resnet": "rvz_resnet_fwd_f32"}
                        .get(getattr(ev, "kernel", ""), "miopen+rvz_nn_bias_act"),
                        "graph": not args.no_graph, "lanes": args.lanes,
+                       "skip_last_eval": args.skip_last_eval,
                        "parallelism": f"games sharded x{world}"},
             # the dominant kernel of a ply (by time per ply) carries "roofline"; the other side
             # of the ply (NN vs search) is reported beside it

@@ -97,6 +97,13 @@ int rvz_search_step(rvz_engine *e, void *leaf_x, int32_t *need);
  * that kernel) or of rvz_search_visits / rvz_tree_export, so policy and value must stay valid and
  * unmodified on the stream until that call. */
 int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, const float *value);
+/* Instead of rvz_search_submit for the LAST batch of a search (after the rvz_search_step that
+ * issued it): leave its leaves unevaluated. The evaluation of the last batch feeds only state the
+ * discarded tree never reads (the leaf's children priors, W along the path; mcts.py:600-640), so
+ * rvz_search_visits / rvz_act then back up the visit counts alone and return exactly the visits,
+ * p and move of the evaluated search (tests/test_gpu_search.py::test_skip_last_eval_bit_exact).
+ * An opt-in optimisation (one NN call fewer per move), not the reference's call sequence. */
+int rvz_search_skip(rvz_engine *e);
 /* {move: child.visit_count} (mcts.py:406-407) as int32 [n_games, S*S+1] */
 int rvz_search_visits(rvz_engine *e, int32_t *out);
 /* get_action_probs' tail (mcts.py:656-692) + SelfPlay's make_move (self_play.py:98):

@@ -225,3 +225,34 @@ def test_bf16_leaf_planes_equal_f32():
     torch.cuda.synchronize()
     assert torch.equal(a.leaf_x, b.leaf_x.float())
     assert torch.equal(a.need, b.need)
+
+
+@pytest.mark.parametrize("board,sims", [(8, 800), (8, 100), (6, 400)])
+def test_skip_last_eval_bit_exact(board, sims):
+    """rvz_search_skip leaves the last batch of every search unevaluated: the visit counts, the
+    f64 policy vectors, the sampled moves and the boards must be bit-identical to the evaluated
+    search over whole games (autoreset keeps every slot busy), with a real network's outputs."""
+    import rvz
+    G, plies = 256, 70
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(board, 2, 64).cuda().eval()
+    runs = []
+    for skip in (False, True):
+        ev = rvz.LeafEvaluator(net)
+        eng = rvz.Engine(G, num_simulations=sims, batch_size=64, board_size=board)
+        run = rvz.SelfPlayRunner(eng, ev, temperature=1.0, autoreset=True, seed_base=7,
+                                 skip_last_eval=skip)
+        run.start()
+        trace = []
+        for _ in range(plies):
+            run.ply()
+            b, w, st = eng.get_state()
+            trace.append((eng.idx_buf.clone(), eng.p_buf.clone(), b.clone(), w.clone(),
+                          st.clone()))
+        eng.check()
+        runs.append((trace, int(run.steps.item()), int(run.games_done.item())))
+    (ta, sa, da), (tb, sb, db) = runs
+    assert sa == sb and da == db and da > 0
+    for k, (x, y) in enumerate(zip(ta, tb)):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v), k
