@@ -135,6 +135,68 @@ def instrumented(run, eng, ev, plies):
     return ms, n, {"step": st, "act": act}
 
 
+def env_bench(device, board=8, n=1 << 23, reps=10):
+    """SURVEY §8d env microbench: the batched rules kernels over n HBM-resident positions (random
+    playouts of 0..40 plies, so every game stage is present), timed with HIP events on the launch
+    stream. Algorithmic bytes per board in this layout (u64 black, u64 white, int32[4] status):
+    legal = 8 + 8 + 4 (side) + 8 (mask out) = 28 B; apply (make_move: legality, flips, auto-pass,
+    terminal, winner) = 8 + 8 + 16 + 4 (square) in, 8 + 8 + 16 + 4 (ok) out = 72 B."""
+    import rvz
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+    B0 = 0x0000000810000000 if board == 8 else 0x0000000408000000
+    W0 = 0x0000001008000000 if board == 8 else 0x0000000810000000
+    black = torch.full((n,), B0, dtype=torch.int64, device=device)
+    white = torch.full((n,), W0, dtype=torch.int64, device=device)
+    status = torch.zeros(n, 4, dtype=torch.int32, device=device)
+    status[:, 0] = 1
+    plies = torch.randint(0, 41, (n,), generator=g, device=device)
+    def lowest_bit(x):                                              # index of the lowest set bit
+        lsb = x & -x
+        f = lsb.to(torch.float64).abs()                             # powers of two are exact
+        return torch.where(lsb < 0, torch.full_like(x, 63), torch.log2(f).round().long())
+
+    def random_legal(mask):
+        """A legal square per board: the first legal square at or after a random start (cyclic;
+        not uniform, enough to spread the positions); -1 (pass) without one."""
+        s0 = torch.randint(0, board * board, (n,), generator=g, device=device)
+        hi = mask & ~((torch.ones_like(mask) << s0) - 1)
+        pick = lowest_bit(torch.where(hi != 0, hi, mask))
+        return torch.where(mask != 0, pick, torch.full_like(pick, -1)).int()
+
+    for k in range(40):
+        sq = random_legal(rvz.board_legal(black, white, status, board))
+        live = (plies > k) & (status[:, 1] == 0) & (sq >= 0)
+        sq = torch.where(live, sq, torch.full_like(sq, -2))        # -2: no move this round
+        rvz.board_apply(black, white, status, sq, board)
+    sq = random_legal(rvz.board_legal(black, white, status, board))
+    copies = [(black.clone(), white.clone(), status.clone()) for _ in range(reps)]
+    torch.cuda.synchronize(device)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = {}
+    rvz.board_legal(black, white, status, board)
+    a.record()
+    for _ in range(reps):
+        rvz.board_legal(black, white, status, board)
+    b.record()
+    torch.cuda.synchronize(device)
+    t = a.elapsed_time(b) / reps * 1e-3
+    out["legal"] = {"boards_per_s": round(n / t), "alg_bytes_per_board": 28,
+                    "achieved_GBs": round(n * 28 / t / 1e9, 1),
+                    "frac": round(n * 28 / t / 1e9 / HBM_PEAK_GBS, 4), "avg_us": round(t * 1e6, 1)}
+    a.record()
+    for cb, cw, cs in copies:
+        rvz.board_apply(cb, cw, cs, sq, board)
+    b.record()
+    torch.cuda.synchronize(device)
+    t = a.elapsed_time(b) / reps * 1e-3
+    out["apply"] = {"plies_per_s": round(n / t), "alg_bytes_per_ply": 72,
+                    "achieved_GBs": round(n * 72 / t / 1e9, 1),
+                    "frac": round(n * 72 / t / 1e9 / HBM_PEAK_GBS, 4), "avg_us": round(t * 1e6, 1)}
+    out["boards"] = n
+    return out
+
+
 def cpu_baseline(args, net):
     """The oracle port (oracle/, literal reference semantics) + the same net in fp32 on the host
     cores, from the start position, over a bounded sample of the C2 workload."""
@@ -177,12 +239,30 @@ def cpu_baseline(args, net):
     while stub.step() is not None:
         stub.submit(u, z)
     dt_stub = time.perf_counter() - t1
+    # the same on ONE core (OpenMP of the oracle library set to 1 thread), 48 searches
+    import ctypes
+    one = None
+    try:
+        gomp = ctypes.CDLL("libgomp.so.1")
+        gomp.omp_set_num_threads(1)
+        G1 = 48
+        stub1 = O.Search(G1, args.sims, args.batch, 1.0, bs=args.board)
+        t2 = time.perf_counter()
+        stub1.begin([O.new_game(args.board) for _ in range(G1)])
+        while stub1.step() is not None:
+            stub1.submit(u[:G1], z[:G1])
+        one = {"value": G1 / (time.perf_counter() - t2), "unit": "board-steps/s", "cores": 1,
+               "sample": f"{G1} first-ply searches, zero-cost evaluator, 1 thread"}
+        gomp.omp_set_num_threads(cores)
+    except OSError:
+        pass
     return {"value": steps / dt, "unit": "board-steps/s", "cores": cores, "kind": "port",
             "sample": f"{G} games from the start position, {steps} plies in {dt:.1f}s, "
                       f"{args.sims} sims, oracle/ C search + {args.blocks}x{args.filters} net "
                       f"fp32 on {cores} host threads",
-            "env_tree_only": {"value": G / dt_stub, "unit": "board-steps/s",
-                              "sample": f"{G} first-ply searches, zero-cost evaluator"}}
+            "env_tree_only": {"value": G / dt_stub, "unit": "board-steps/s", "cores": cores,
+                              "sample": f"{G} first-ply searches, zero-cost evaluator"},
+            "env_tree_only_1core": one}
 
 
 def main():
@@ -291,6 +371,7 @@ def main():
     search_ms_per_ply = kernels[dom]["avg_us"] * kernels[dom]["launches_per_ply"] / 1e3
     nn_dominant = ms.get("nn_trunk", ms["nn"]) * nn_per_ply > search_ms_per_ply
 
+    envb = env_bench(device, args.board) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, net)
@@ -328,6 +409,7 @@ def main():
             "search_roofline" if nn_dominant else "nn_roofline":
                 search_roof if nn_dominant else nn_roof,
             "kernels": {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()},
+            "env_roofline": envb,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
