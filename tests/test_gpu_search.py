@@ -256,3 +256,35 @@ def test_skip_last_eval_bit_exact(board, sims):
     for k, (x, y) in enumerate(zip(ta, tb)):
         for u, v in zip(x, y):
             assert torch.equal(u, v), k
+
+
+def test_lanes_play_the_same_games():
+    """rvz.LaneRunner (two independent lanes on forked streams, captured into one HIP graph)
+    plays exactly the games of one SelfPlayRunner over the same global game indices: moves,
+    policy vectors and boards bit-identical ply by ply, autoreset included."""
+    import rvz
+    G, plies, sims = 256, 64, 200
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 2, 64).cuda().eval()
+
+    def make_eng(n):
+        return rvz.Engine(n, num_simulations=sims, batch_size=64)
+
+    one = rvz.SelfPlayRunner(make_eng(G), rvz.LeafEvaluator(net), autoreset=True, seed_base=11)
+    two = rvz.LaneRunner(make_eng, lambda: rvz.LeafEvaluator(net), G, lanes=2, autoreset=True,
+                         seed_base=11)
+    one.start()
+    two.start()
+    for k in range(plies):
+        for r in (one, two):
+            r.ply()
+            if k == 0:
+                r.capture()         # first ply eager, the rest replayed from the graph
+        la, lb = two.runners
+        assert torch.equal(one.eng.idx_buf, torch.cat([la.eng.idx_buf, lb.eng.idx_buf])), k
+        assert torch.equal(one.eng.p_buf, torch.cat([la.eng.p_buf, lb.eng.p_buf])), k
+        b1 = one.eng.get_state()[0].clone()
+        b2 = torch.cat([la.eng.get_state()[0], lb.eng.get_state()[0]])
+        assert torch.equal(b1, b2), k
+    assert int(one.steps.item()) == int(two.steps.item())
+    assert int(one.games_done.item()) == int(two.games_done.item()) > 0
