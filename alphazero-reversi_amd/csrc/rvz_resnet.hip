@@ -209,7 +209,7 @@ __device__ __forceinline__ void stem(const float* xin, const Act& act, const flo
 // (cells = BS*BS), hpv(b)[0 .. 2 cells) = the policy planes (NCHW flatten, the FC's input order)
 // and hpv(b)[2 cells .. 3 cells) = the value plane. A BS < 8 board sits in the top-left corner
 // of the 8x8 pixel grid.
-template <int F, int NBOARD, int NTHR, int BS = 8, class Act, class Out>
+template <int F, int NBOARD, int NTHR, int BS = 8, bool PACKED = false, class Act, class Out>
 __device__ __forceinline__ void head_convs(const Act& act, float* part,
                                            const float* __restrict__ prm, const Layout& L,
                                            const Out& hpv, int tid) {
@@ -218,15 +218,19 @@ __device__ __forceinline__ void head_convs(const Act& act, float* part,
     const int lane = tid & 63;
     {
         const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        // PACKED: board b's cells are act rows b * BS^2 + cell (h2); else the 8x8 grid
         const int b = wave % NBOARD, cg = wave / NBOARD, row = b * 64 + lane;
+        const int arow = PACKED ? b * BS * BS + lane : row;
+        const bool on = !PACKED || lane < BS * BS;
         const float* w0 = prm + L.pol_w + cg * CPG;
         const float* w1 = w0 + F;
         const float* w2 = prm + L.val_w + cg * CPG;
         float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
 #pragma unroll
         for (int k8 = 0; k8 < CPG / 8; ++k8) {
+            if (!on) break;
             float v[8];
-            act.load8(row, cg * CPG + 8 * k8, v);
+            act.load8(arow, cg * CPG + 8 * k8, v);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 p0 = fmaf(v[j], w0[8 * k8 + j], p0);
@@ -243,7 +247,7 @@ __device__ __forceinline__ void head_convs(const Act& act, float* part,
     for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
         const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
         const int b = rem / CELLS, cell = rem % CELLS;
-        const int row = b * 64 + (cell / BS) * 8 + cell % BS;      // pixel of the 8x8 grid
+        const int row = b * 64 + (PACKED ? cell : (cell / BS) * 8 + cell % BS);
         float acc = 0.0f;
 #pragma unroll
         for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * NBOARD * 64 + row];
@@ -1193,20 +1197,41 @@ __device__ __forceinline__ float h16f(uint16_t h) {
     return (float)__builtin_bit_cast(_Float16, h);
 }
 
-template <int F, int NBOARD>
+// Board geometry of a workgroup: NB boards of BS x BS cells packed row-major, pixel row
+// px = b * BS^2 + r * BS + c (8x8: b * 64 + r * 8 + c; a 6x6 board takes 36 rows, not the 64 of
+// an embedding in the 8x8 grid), rounded up to whole 16-pixel MFMA tiles; rows past the boards
+// are padding (no valid tap, never read), up to a multiple of RND (whole pixel tiles for every
+// wave: 16 x the waves along the pixels).
+template <int NB, int BS, int RND>
+struct GeoH {
+    static constexpr int PPB = BS * BS;
+    static constexpr int NVALID = NB * PPB;
+    static constexpr int NPIX = (NVALID + RND - 1) / RND * RND;
+    // the 3x3 taps of pixel px that stay on its board (bit t = tap (t/3 - 1, t%3 - 1))
+    static __device__ __forceinline__ unsigned taps(int px) {
+        const int cell = px % PPB, r = cell / BS, c = cell % BS;
+        unsigned m = 0;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            if ((unsigned)(r + t / 3 - 1) < (unsigned)BS && (unsigned)(c + t % 3 - 1) < (unsigned)BS)
+                m |= 1u << t;
+        return px < NVALID ? m : 0u;
+    }
+    static __device__ __forceinline__ int tap_offset(int t) { return (t / 3 - 1) * BS + (t % 3 - 1); }
+};
+
+template <int F, int NPIX>
 struct CfgH {
-    static constexpr int ZROW = NBOARD * 64;
+    static constexpr int ZROW = NPIX;                // first of the 8 zero rows
     static constexpr int KS = F / H2_K;              // k-step planes of 32 channels
     static constexpr int KSP = (ZROW + 8) * H2_K;    // halves per k-step plane
     static constexpr int PLANE = KS * KSP;           // halves per part
     static constexpr int ACT = 2 * PLANE;            // halves per buffer
-    static constexpr int XIN = NBOARD * 100 * 4;     // floats, aliased onto buffer B
     static constexpr int BYTES = 2 * ACT * 2;
     static constexpr int NIT = 9 * KS;
     static constexpr int CT = F / H2_TM;
-    static_assert(XIN * 4 <= ACT * 2, "xin fits in buffer B");
     static_assert((PLANE * 2) % 16 == 0 && (KSP * 2) % 16 == 0, "16-byte aligned planes");
-    static_assert(BYTES * RVZ_H2_OCC <= 160 * 1024 || NBOARD == 1, "LDS for the occupancy");
+    static_assert(BYTES <= 160 * 1024, "fits the LDS of a CU");
     // halves offset of (row, k-step plane ks, 8-channel slot q in 0..3)
     static __device__ __forceinline__ int at(int row, int ks, int q) {
         return ks * KSP + row * H2_K + 8 * (q ^ ((row >> 1) & 3));
@@ -1214,14 +1239,14 @@ struct CfgH {
 };
 
 // activation reader for the heads (join of the two parts)
-template <int F, int NBOARD>
+template <int F, int NPIX>
 struct ActH2 {
     const uint16_t* p;
     __device__ void load8(int row, int k0, float (&v)[8]) const {
         typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
-        const int o = CfgH<F, NBOARD>::at(row, k0 / H2_K, (k0 % H2_K) >> 3);
+        const int o = CfgH<F, NPIX>::at(row, k0 / H2_K, (k0 % H2_K) >> 3);
         const u16x8 a = *reinterpret_cast<const u16x8*>(p + o);
-        const u16x8 b = *reinterpret_cast<const u16x8*>(p + CfgH<F, NBOARD>::PLANE + o);
+        const u16x8 b = *reinterpret_cast<const u16x8*>(p + CfgH<F, NPIX>::PLANE + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = h16f(a[j]) + h16f(b[j]);
     }
@@ -1265,12 +1290,12 @@ __device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __rest
 
 // v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
 // channels of one pixel per tile -> two 8-byte writes
-template <int F, int NBOARD, int CTW, int PTW, bool RES, bool KEEP>
+template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP>
 __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                                             const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
                                             const WaveTilesH<F, CTW, PTW>& wt, int lane,
                                             bool& ovf) {
-    using C = CfgH<F, NBOARD>;
+    using C = CfgH<F, NPIX>;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
     typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
@@ -1346,7 +1371,7 @@ __device__ __forceinline__ void stem_h2_load(const uint16_t* __restrict__ blob,
 
 // the stem's operands are loaded up front (stem_h2_load, with the leaf planes): one global
 // round trip before the first MFMA instead of three dependent ones
-template <int F, int NBOARD, int CTW, int PTW>
+template <int F, int NBOARD, int CTW, int PTW, int BS>
 __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__ out,
                                         const f16x8 (&w)[CTW][2], int wave, int lane,
                                         EpiH<CTW, PTW>& er, bool& ovf) {
@@ -1355,7 +1380,9 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
     f16x8 a[PTW][2];
 #pragma unroll
     for (int u = 0; u < PTW; ++u) {
-        const int px = wt.px[u], b = px >> 6, r = (px & 63) >> 3, cc = px & 7;
+        using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
+        const int px = wt.px[u], b = px / G::PPB, r = (px % G::PPB) / BS, cc = px % BS;
+        const bool on = px < G::NVALID;               // padding rows: zero input
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 h0, h1;
 #pragma unroll
@@ -1364,7 +1391,8 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const int k = kq + 2 * i + e, t = k / 3, ch = k % 3;
-                xv[e] = k < 27 ? xin[(b * 100 + (r + t / 3) * 10 + (cc + t % 3)) * 4 + ch] : 0.0f;
+                xv[e] = k < 27 && on ? xin[(b * 100 + (r + t / 3) * 10 + (cc + t % 3)) * 4 + ch]
+                                     : 0.0f;
             }
             uint32_t p0, p1;
             split2x2(xv, p0, p1);
@@ -1389,7 +1417,7 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 #endif
     }
     STEM_T(5);
-    epilogue_h2<F, NBOARD, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
 }
 
 template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS>
@@ -1399,22 +1427,15 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
                                         const float* __restrict__ isc, int wave, int lane,
                                         f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
                                         bool& ovf) {
-    using C = CfgH<F, NBOARD>;
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
+    using C = CfgH<F, G::NPIX>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
     const WaveTilesH<F, CTW, PTW> wt(wave, lane);
     load_epi(er, bias, isc, wt, lane);                // lands during the k-loop
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
     unsigned pmask[PTW];
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-        const int rr = (wt.px[u] & 63) >> 3, cc = wt.px[u] & 7;
-        unsigned msk = 0;
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-            if ((unsigned)(rr + t / 3 - 1) < (unsigned)BS && (unsigned)(cc + t % 3 - 1) < (unsigned)BS)
-                msk |= 1u << t;
-        pmask[u] = msk;
-    }
+    for (int u = 0; u < PTW; ++u) pmask[u] = G::taps(wt.px[u]);
     f32x4 acc[CTW][PTW];
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
@@ -1429,7 +1450,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     };
     auto load_a = [&](f16x8 (&aq)[PTW][2], int it) {
         const int t = it / KS, ks = it - t * KS;
-        const int off = (t / 3 - 1) * 8 + (t % 3 - 1);
+        const int off = G::tap_offset(t);
 #pragma unroll
         for (int u = 0; u < PTW; ++u) {
             const int nat = wt.px[u] + off;
@@ -1465,7 +1486,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
 #pragma unroll
             for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
     // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
-    epilogue_h2<F, NBOARD, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
 }
 
 // the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for
@@ -1500,10 +1521,12 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, float* __restrict__ logits,
                  float* __restrict__ value) {
-    using C = CfgH<F, NBOARD>;
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
+    using C = CfgH<F, G::NPIX>;
     using WT = WaveTilesH<F, CTW, PTW>;
-    static_assert(WT::CG * (NBOARD * 64 / (PTW * H2_TN)) == 4, "4 waves");
+    static_assert(WT::CG * (G::NPIX / (PTW * H2_TN)) == 4, "4 waves");
     static_assert((1024 + NBOARD * (192 + 256)) * 4 <= C::ACT * 2, "heads scratch fits in B");
+    static_assert(NBOARD * 100 * 4 * 4 <= C::ACT * 2, "xin fits in buffer B");
     constexpr int NTHR = 256;
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
     uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
@@ -1542,7 +1565,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     STEM_T(1);
     __syncthreads();
     STEM_T(2);
-    stem_h2<F, NBOARD, CTW, PTW>(xin, actA, ws, wave, lane, er, ovf);
+    stem_h2<F, NBOARD, CTW, PTW, BS>(xin, actA, ws, wave, lane, er, ovf);
     STEM_T(3);
     __syncthreads();
     PHASE(1);
@@ -1566,12 +1589,14 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         float* part = reinterpret_cast<float*>(actB);
         float* hpv = part + 1024;
         float* h1 = hpv + NBOARD * 192;
-        head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, part, prm, L, HeadsLds{hpv}, tid);
+        head_convs<F, NBOARD, NTHR, BS, true>(ActH2<F, G::NPIX>{actA}, part, prm, L, HeadsLds{hpv},
+                                              tid);
         __syncthreads();
         head_fcs<NBOARD, NTHR, BS>(hpv, h1, prm, L, g0, n_boards, logits, value, tid);
     } else {
-        head_convs<F, NBOARD, NTHR, BS>(ActH2<F, NBOARD>{actA}, reinterpret_cast<float*>(actB), prm,
-                                        L, HeadsGlobal{work, g0, n_boards}, tid);
+        head_convs<F, NBOARD, NTHR, BS, true>(ActH2<F, G::NPIX>{actA},
+                                              reinterpret_cast<float*>(actB), prm, L,
+                                              HeadsGlobal{work, g0, n_boards}, tid);
     }
     PHASE(3);
     RT(1);
@@ -1642,11 +1667,6 @@ static void launch_trunk(const float* x, int32_t n, const float* params, const u
                            dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
 }
 
-// F = 64: RVZ_H2_NB64 boards per workgroup — 2 (2 x 4 tiles per wave, 2 workgroups per CU) or
-// 1 (2 x 2 tiles per wave, 4 workgroups per CU)
-#ifndef RVZ_H2_NB64
-#define RVZ_H2_NB64 2
-#endif
 template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
                             int32_t filters, int32_t blocks, float* work, float* logits,
@@ -1655,15 +1675,19 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
 #endif
-    if (filters == 64 && RVZ_H2_NB64 == 2)
-        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, BS, 2>), dim3((n + 1) / 2), dim3(256),
+    if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
+        if (filters == 64)
+            hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), dim3((n + 3) / 4), dim3(256), 0, s,
+                               x, n, params, L, blob, blocks, work, logits, value);
+        else
+            hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), dim3(n), dim3(256), 0, s, x, n,
+                               params, L, blob, blocks, work, logits, value);
+    } else if (filters == 64)
+        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), dim3((n + 1) / 2), dim3(256),
                            RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value);
-    else if (filters == 64)
-        hipLaunchKernelGGL((k_resnet_h2<64, 1, 2, 2, BS, 4>), dim3(n), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work, logits, value);
     else
-        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, BS, 2>), dim3(n), dim3(256), 0, s, x, n, params,
-                           L, blob, blocks, work, logits, value);
+        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), dim3(n), dim3(256), 0, s, x, n,
+                           params, L, blob, blocks, work, logits, value);
 }
 
 extern "C" {

@@ -298,11 +298,16 @@ class LeafEvaluator:
 
     def mfma_flops_per_row(self) -> int:
         """FLOPs the trunk kernel executes on the 16-bit matrix cores per board, stem K padded
-        27 -> 32, over the 8x8 pixel grid (a 6x6 board is computed embedded in it): three
-        partial products per fp32 product for h2 (f16 MFMA), six for split (bf16 MFMA)."""
-        cells, f = 64, self.filters
+        27 -> 32: three partial products per fp32 product for h2 (f16 MFMA), six for split
+        (bf16 MFMA). Pixel rows per board: 64 on 8x8; a 6x6 board is packed by h2 (4 boards in
+        160 rows at 64 filters, 1 in 48 at 128) and embedded in the 8x8 grid by split."""
+        f = self.filters
+        if self.board_size == 8 or self.kernel != "h2":
+            rows = 64
+        else:
+            rows = 40 if f == 64 else 48
         terms = 3 if self.kernel == "h2" else 6
-        return terms * 2 * cells * f * (32 + 2 * self.n_blocks * 9 * f)
+        return terms * 2 * rows * f * (32 + 2 * self.n_blocks * 9 * f)
 
     @torch.no_grad()
     def __call__(self, x: torch.Tensor):
