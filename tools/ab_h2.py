@@ -24,29 +24,30 @@ for name in names:
     lib = C.CDLL(os.path.join(ROOT, "tools", "_ab", f"librvz_{name}.so"))
     lib.rvz_resnet_h2_size.restype = C.c_int64
     libs.append((name, lib))
+BS = int(os.environ.get("BOARD", 8))
 torch.manual_seed(0)
-net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
+net = rvz.AlphaZeroNetwork(BS, blocks, filters).cuda().eval()
 ev = rvz.LeafEvaluator(net, kernel="h2")
-x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
+x = (torch.rand(n, 3, BS, BS, device="cuda") > 0.6).float()
 s = C.c_void_p(_lib.stream_handle())
 P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
 bufs = {}
 for name, lib in libs:
     blob = torch.empty(lib.rvz_resnet_h2_size(filters, blocks), dtype=torch.int16, device="cuda")
     assert lib.rvz_resnet_h2_weights(P(ev.params), filters, blocks, P(blob), s) == 0
-    bufs[name] = (blob, torch.empty(n, 65, device="cuda"), torch.empty(n, device="cuda"),
+    bufs[name] = (blob, torch.empty(n, BS * BS + 1, device="cuda"), torch.empty(n, device="cuda"),
                   torch.zeros(n * 192 + 4, device="cuda"))
 
 
 def fwd(name, lib):
     blob, lg, v, wk = bufs[name]
-    assert lib.rvz_resnet_fwd_h2(8, P(x), n, P(ev.params), P(blob), filters, blocks, P(wk), P(lg),
+    assert lib.rvz_resnet_fwd_h2(BS, P(x), n, P(ev.params), P(blob), filters, blocks, P(wk), P(lg),
                                  P(v), s) == 0
 
 
 def trunk(name, lib):
     blob, lg, v, wk = bufs[name]
-    assert lib.rvz_resnet_trunk_h2(8, P(x), n, P(ev.params), P(blob), filters, blocks, P(wk),
+    assert lib.rvz_resnet_trunk_h2(BS, P(x), n, P(ev.params), P(blob), filters, blocks, P(wk),
                                    s) == 0
 
 
