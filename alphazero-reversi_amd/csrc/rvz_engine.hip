@@ -584,17 +584,13 @@ __global__ __launch_bounds__(256) void k_act(View v, int expand, const float* __
 }
 
 // reset: new game (board.py:25-39) + np.random.seed(seed) random_sample() stream.
+// a fresh game g seeded with `seed` (np.random.seed semantics): MT19937 init, its first draws,
+// the start position (one wave; k is the wave's 624-word key scratch in LDS)
 template <int BS>
-__global__ __launch_bounds__(256) void k_reset(View v, const uint32_t* __restrict__ seeds,
-                                               const uint8_t* __restrict__ mask) {
-    __shared__ uint32_t key[WPB][624];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int g = blockIdx.x * WPB + wid;
-    if (g >= v.G) return;
-    if (mask && !mask[g]) return;
-    uint32_t* k = key[wid];
+__device__ __forceinline__ void reset_game(const View& v, int g, int lane, uint32_t seed,
+                                           uint32_t* k) {
     if (lane == 0) {  // mt19937_seed (init_genrand): inherently sequential
-        uint32_t sd = seeds[g];
+        uint32_t sd = seed;
         for (int pos = 0; pos < 624; ++pos) {
             k[pos] = sd;
             sd = 1812433253u * (sd ^ (sd >> 30)) + (uint32_t)(pos + 1);
@@ -623,6 +619,43 @@ __global__ __launch_bounds__(256) void k_reset(View v, const uint32_t* __restric
         v.rng_pos[g] = 0;
         v.pend[g] = 0;
     }
+}
+
+template <int BS>
+__global__ __launch_bounds__(256) void k_reset(View v, const uint32_t* __restrict__ seeds,
+                                               const uint8_t* __restrict__ mask) {
+    __shared__ uint32_t key[WPB][624];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = blockIdx.x * WPB + wid;
+    if (g >= v.G) return;
+    if (mask && !mask[g]) return;
+    reset_game<BS>(v, g, lane, seeds[g], key[wid]);
+}
+
+// The self-play driver's per-ply bookkeeping in one launch (SelfPlayRunner, self_play.py:80-101
+// run back to back): plies[g] += (idx[g] >= 0) (a move was committed); when `reset`, a game that
+// just ended counts in done[g], takes its slot's next seed (seeds[g] += stride) and restarts from
+// the start position with it. Per-game counters: no contended atomics; the totals are summed
+// when read.
+template <int BS>
+__global__ __launch_bounds__(256) void k_autoreset(View v, const int32_t* __restrict__ idx,
+                                                   int64_t* __restrict__ seeds, int64_t stride,
+                                                   int64_t* __restrict__ plies,
+                                                   int64_t* __restrict__ done, int reset) {
+    __shared__ uint32_t key[WPB][624];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = blockIdx.x * WPB + wid;
+    if (g >= v.G) return;
+    if (lane == 0 && idx[g] >= 0) plies[g] += 1;
+    if (!reset || !v.status[4 * g + 1]) return;
+    int64_t sd = 0;
+    if (lane == 0) {
+        done[g] += 1;
+        sd = seeds[g] + stride;
+        seeds[g] = sd;
+    }
+    sd = __shfl(sd, 0);
+    reset_game<BS>(v, g, lane, (uint32_t)(sd & 0xFFFFFFFFll), key[wid]);
 }
 
 // ---- board kernels on caller arrays (one thread per board) --------------------------------------
@@ -887,6 +920,16 @@ int rvz_env_reset(rvz_engine* e, const uint32_t* seeds, const uint8_t* mask) {
     else hipLaunchKernelGGL(k_reset<6>, grid, block, 0, e->stream, e->v, seeds, mask);
     e->searching = 0;
     return launch_check(e, "k_reset");
+}
+
+int rvz_env_autoreset(rvz_engine* e, const int32_t* idx, int64_t* seeds, int64_t stride,
+                      int64_t* plies, int64_t* done, int32_t reset) {
+    if (!e || !idx || !plies || (reset && (!seeds || !done))) return RVZ_EINVAL;
+    if (reset) e->pending = 0;
+    dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
+    if (e->BS == 8) hipLaunchKernelGGL(k_autoreset<8>, grid, block, 0, e->stream, e->v, idx, seeds, stride, plies, done, reset);
+    else hipLaunchKernelGGL(k_autoreset<6>, grid, block, 0, e->stream, e->v, idx, seeds, stride, plies, done, reset);
+    return launch_check(e, "k_autoreset");
 }
 
 int rvz_env_get(rvz_engine* e, uint64_t* black, uint64_t* white, int32_t* status) {

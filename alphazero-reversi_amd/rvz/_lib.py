@@ -52,6 +52,7 @@ SIGNATURES = {
     "rvz_search_begin": (C.c_int, [_P]),
     "rvz_search_step": (C.c_int, [_P, _P, _P]),
     "rvz_search_submit": (C.c_int, [_P, _P, C.c_int32, _P]),
+    "rvz_env_autoreset": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P, C.c_int32]),
     "rvz_search_skip": (C.c_int, [_P]),
     "rvz_search_visits": (C.c_int, [_P, _P]),
     "rvz_act": (C.c_int, [_P, C.c_double, _P, C.c_int32, _P, _P]),

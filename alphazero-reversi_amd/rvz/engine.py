@@ -155,6 +155,18 @@ class Engine:
         self._stream()
         self._call("rvz_env_reset", ptr(seeds_i32), ptr(mask_u8) if mask_u8 is not None else None)
 
+    def autoreset(self, idx: torch.Tensor, seeds: torch.Tensor, stride: int,
+                  plies: torch.Tensor, done: torch.Tensor, reset: bool = True):
+        """rvz_env_autoreset: count committed plies per game; restart finished games with their
+        slot's next seed (seeds int64 [G] advanced in place by stride). Graph-capturable."""
+        for t, dt in ((idx, torch.int32), (seeds, torch.int64), (plies, torch.int64),
+                      (done, torch.int64)):
+            if t.dtype != dt or t.numel() != self.n_games or not t.is_contiguous():
+                raise RvzError("autoreset: idx int32, seeds/plies/done int64, [n_games]")
+        self._stream()
+        self._call("rvz_env_autoreset", ptr(idx), ptr(seeds), int(stride), ptr(plies), ptr(done),
+                   int(bool(reset)))
+
     def get_state(self):
         """(black int64[G], white int64[G], status int32[G,4]) device tensors (bit patterns)."""
         self._stream()

@@ -28,9 +28,12 @@ class SelfPlayRunner:
     def __init__(self, engine: Engine, evaluator: Callable, temperature: float = 1.0,
                  fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
                  record: bool = False, max_plies: int = 60, seed_stride: int = None,
-                 skip_last_eval: bool = False):
+                 skip_last_eval: bool = False, fused_bookkeeping: bool = True):
         self.eng = engine
         self.skip_last_eval = bool(skip_last_eval)
+        # fused_bookkeeping: ply counting and autoreset in one engine kernel (rvz_env_autoreset)
+        # instead of ~12 small torch kernels per ply; the games are the same either way
+        self.fused_bookkeeping = bool(fused_bookkeeping)
         self.evaluator = evaluator
         self.temperature = float(temperature)
         self.fused_softmax = fused_softmax
@@ -40,8 +43,8 @@ class SelfPlayRunner:
         self.record = record
         G, dev = engine.n_games, engine.device
         self.seeds = (torch.arange(G, dtype=torch.int64, device=dev) + seed_base)
-        self.steps = torch.zeros((), dtype=torch.int64, device=dev)   # committed plies
-        self.games_done = torch.zeros((), dtype=torch.int64, device=dev)
+        self._plies = torch.zeros(G, dtype=torch.int64, device=dev)   # committed plies per slot
+        self._done = torch.zeros(G, dtype=torch.int64, device=dev)    # finished games per slot
         self.pre_black = torch.zeros(G, dtype=torch.int64, device=dev)
         self.pre_white = torch.zeros(G, dtype=torch.int64, device=dev)
         self.pre_status = torch.zeros(G, 4, dtype=torch.int32, device=dev)
@@ -58,6 +61,15 @@ class SelfPlayRunner:
             self.rec_over = torch.zeros(max_plies, G, 4, dtype=torch.int32, device=dev)
         self.ply_index = 0
 
+    @property
+    def steps(self) -> torch.Tensor:
+        """Committed plies (board-steps) over all slots, a 0-d device tensor."""
+        return self._plies.sum()
+
+    @property
+    def games_done(self) -> torch.Tensor:
+        return self._done.sum()
+
     def start(self):
         self.eng.reset(self.seeds)
         self.ply_index = 0
@@ -65,23 +77,29 @@ class SelfPlayRunner:
     # one ply for every game; graph-capturable (no host sync)
     def _body(self):
         eng = self.eng
-        b, w, st = eng.get_state()
-        self.pre_black.copy_(b)
-        self.pre_white.copy_(w)
-        self.pre_status.copy_(st)
+        if self.record:          # the states before the move, for the game records
+            b, w, st = eng.get_state()
+            self.pre_black.copy_(b)
+            self.pre_white.copy_(w)
+            self.pre_status.copy_(st)
         eng.search(self.evaluator, fused_softmax=self.fused_softmax,
                    skip_last_eval=self.skip_last_eval)
         idx, _ = eng.act(self.temperature, apply=True)
-        self.steps += (idx >= 0).sum()
-        _, _, st = eng.get_state()
-        self.post_status.copy_(st)
+        if self.record:
+            self.post_status.copy_(eng.get_state()[2])
+        if self.fused_bookkeeping:
+            eng.autoreset(idx, self.seeds, self.seed_stride, self._plies, self._done,
+                          reset=self.autoreset)
+            return
+        self._plies += (idx >= 0).to(torch.int64)
         if self.autoreset:
-            self.restart_finished(st)
+            self.restart_finished(eng.get_state()[2])
 
     def restart_finished(self, status: torch.Tensor):
-        """Restart games that just ended with the next seed of their slot (graph-capturable)."""
+        """Restart games that just ended with the next seed of their slot (graph-capturable;
+        the torch form of rvz_env_autoreset's reset)."""
         over = status[:, 1]
-        self.games_done += over.sum()
+        self._done += over.to(torch.int64)
         self.seeds += over.to(torch.int64) * self.seed_stride
         self._mask.copy_(over.to(torch.uint8))
         self._seed32.copy_(self.seeds.bitwise_and(0xFFFFFFFF).to(torch.int32))

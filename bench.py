@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--skip-last-eval", action="store_true",
                     help="leave each search's last batch unevaluated (rvz_search_skip): "
                          "bit-identical games, one NN call fewer per move; off for the headline")
+    ap.add_argument("--torch-bookkeeping", action="store_true",
+                    help="per-ply counting / autoreset as torch ops instead of rvz_env_autoreset")
     ap.add_argument("--lanes", type=int, default=1,
                     help="independent game lanes per GPU, one stream each in one graph "
                          "(rvz.LaneRunner); the games are the same as with one lane")
@@ -302,7 +304,8 @@ def main():
                                          fused_softmax=True, autoreset=True,
                                          seed_base=args.seed + first_game,
                                          seed_stride=args.games * world,
-                                         skip_last_eval=args.skip_last_eval)
+                                         skip_last_eval=args.skip_last_eval,
+                                         fused_bookkeeping=not args.torch_bookkeeping)
         engines = [run.eng]
     eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
     run.start()

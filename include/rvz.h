@@ -64,6 +64,13 @@ int rvz_version(void);
  * MT19937 stream with seeds[g] (np.random.seed, the RNG behind mcts.py:684). mask: reset only
  * games with mask[g] != 0 (NULL = all). */
 int rvz_env_reset(rvz_engine *e, const uint32_t *seeds, const uint8_t *mask);
+/* The self-play loop's per-ply bookkeeping (self_play.py:80-101 with every game slot kept busy):
+ * plies[g] += 1 when idx[g] >= 0 (rvz_act committed a move); with reset != 0 a game that is over
+ * adds 1 to done[g], takes seeds[g] += stride (int64, in place) and restarts from the start
+ * position with np.random.seed(seeds[g] mod 2^32) semantics, as rvz_env_reset. idx: rvz_act's
+ * out_idx; plies, done: int64 [n_games] per-game counters (sum them to read totals). */
+int rvz_env_autoreset(rvz_engine *e, const int32_t *idx, int64_t *seeds, int64_t stride,
+                      int64_t *plies, int64_t *done, int32_t reset);
 int rvz_env_get(rvz_engine *e, uint64_t *black, uint64_t *white, int32_t *status);
 int rvz_env_set(rvz_engine *e, const uint64_t *black, const uint64_t *white, const int32_t *status);
 /* ReversiGame.get_valid_moves (game.py:72-79 -> board.py:70-133) as a bitmask per game */

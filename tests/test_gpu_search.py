@@ -288,3 +288,31 @@ def test_lanes_play_the_same_games():
         assert torch.equal(b1, b2), k
     assert int(one.steps.item()) == int(two.steps.item())
     assert int(one.games_done.item()) == int(two.games_done.item()) > 0
+
+
+def test_fused_bookkeeping_matches_torch_path():
+    """rvz_env_autoreset (ply counting + restart of finished games with their slot's next seed,
+    one kernel) against the torch form (restart_finished + rvz_env_reset): the same games,
+    seeds, boards and counters, over enough plies that many games end and restart."""
+    import rvz
+    G, plies, sims = 128, 75, 128     # 2 batches: at 64 the root's children stay unvisited
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
+    runs = []
+    for fused in (True, False):
+        eng = rvz.Engine(G, num_simulations=sims, batch_size=64)
+        run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=3,
+                                 seed_stride=1000, fused_bookkeeping=fused)
+        run.start()
+        trace = []
+        for _ in range(plies):
+            run.ply()
+            b, w, st = eng.get_state()
+            trace.append((eng.idx_buf.clone(), b.clone(), w.clone(), st.clone(),
+                          run.seeds.clone()))
+        runs.append((trace, int(run.steps.item()), int(run.games_done.item())))
+    (ta, sa, da), (tb, sb, db) = runs
+    assert sa == sb and da == db and da >= G
+    for k, (x, y) in enumerate(zip(ta, tb)):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v), k
