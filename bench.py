@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--config", choices=sorted(PRESETS), default="c2",
                     help="BASELINE.json workload preset; explicit flags override it")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=60,
+                    help="timed plies; the default spans a whole 8x8 game (every stage, endgame "
+                         "included): the steady-state mix of continuous self-play")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--games", type=int, default=None, help="games per GPU")
     ap.add_argument("--sims", type=int, default=None)
@@ -94,14 +96,16 @@ def make_net(args, device):
 
 
 def instrumented(run, eng, ev, plies):
-    """Eager plies with the engine's launch timing on (a HIP event pair, without system fence,
-    around every k_step / k_act on the launch stream) and the kernels' own algorithmic-byte
-    counters. Each ply is enqueued behind a device-side sleep so the host runs ahead of the GPU
-    and the intervals bracket only the kernels. The NN is timed separately (back-to-back calls)."""
-    eng.stats_enable(True)
-    eng.timing_enable(True)
+    """Eager plies, first with the engine's launch timing on (a HIP event pair, without system
+    fence, around every k_step / k_act on the launch stream), then as many with the kernels'
+    own algorithmic-byte counters on (per-game counter writes slow the search kernels, so they
+    are never on while timing; both cover the same launches per ply). Each ply is enqueued
+    behind a device-side sleep so the host runs ahead of the GPU and the intervals bracket only
+    the kernels. The NN is timed separately (back-to-back calls)."""
     nn_calls = 0
-    for _ in range(plies):
+
+    def one_ply():
+        nonlocal nn_calls
         torch.cuda.synchronize(eng.device)
         torch.cuda._sleep(int(60e6))        # ~25-30 ms of device time: the host enqueues meanwhile
         eng.search_begin()
@@ -111,10 +115,18 @@ def instrumented(run, eng, ev, plies):
             nn_calls += 1
         eng.act(run.temperature, apply=True)
         run.restart_finished(eng.get_state()[2])
+
+    eng.timing_enable(True)
+    for _ in range(plies):
+        one_ply()
     t = eng.timing_read()
     eng.timing_enable(False)
+    eng.stats_enable(True)
+    for _ in range(plies):
+        one_ply()
     st, act, _ = eng.stats_read()
     eng.stats_enable(False)
+    nn_calls //= 2
     # evaluator: 10 back-to-back calls on the same leaf tensor between two events
     stream = torch.cuda.current_stream(eng.device)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
