@@ -1102,6 +1102,47 @@ int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, i
     return launch_check(e, "k_act");
 }
 
+// ---- stream-ordered HIP event timer without system fence (bench.py: per-launch kernel
+// durations in eager plies; torch's events carry a system-scope fence that adds tens of us)
+struct rvz_timer {
+    std::vector<hipEvent_t> ev;
+};
+
+int rvz_timer_create(int32_t n, rvz_timer** out) {
+    if (n <= 0 || !out) return RVZ_EINVAL;
+    rvz_timer* t = new rvz_timer;
+    t->ev.resize(n, nullptr);
+    for (auto& e : t->ev) {
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) {
+            for (auto& f : t->ev)
+                if (f) (void)hipEventDestroy(f);
+            delete t;
+            return RVZ_EHIP;
+        }
+    }
+    *out = t;
+    return RVZ_OK;
+}
+
+int rvz_timer_record(rvz_timer* t, int32_t i, void* stream) {
+    if (!t || i < 0 || i >= (int32_t)t->ev.size()) return RVZ_EINVAL;
+    return hipEventRecord(t->ev[i], (hipStream_t)stream) == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_timer_elapsed(rvz_timer* t, int32_t i, int32_t j, float* ms) {
+    if (!t || !ms || i < 0 || j < 0 || i >= (int32_t)t->ev.size() || j >= (int32_t)t->ev.size())
+        return RVZ_EINVAL;
+    if (hipEventSynchronize(t->ev[j]) != hipSuccess) return RVZ_EHIP;
+    return hipEventElapsedTime(ms, t->ev[i], t->ev[j]) == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+void rvz_timer_destroy(rvz_timer* t) {
+    if (!t) return;
+    for (auto& e : t->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete t;
+}
+
 int rvz_counters(const rvz_engine* e, int64_t* out2) {
     if (!e || !out2) return RVZ_EINVAL;
     out2[0] = e->counters[0];

@@ -1520,7 +1520,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, float* __restrict__ logits,
-                 float* __restrict__ value) {
+                 float* __restrict__ value, uint64_t* __restrict__ stamps) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
     using C = CfgH<F, G::NPIX>;
     using WT = WaveTilesH<F, CTW, PTW>;
@@ -1536,6 +1536,9 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = blockIdx.x * NBOARD;
     bool ovf = false;
+    // optional device timestamps (bench.py: the launch's span inside a replayed HIP graph):
+    // s_memrealtime (100 MHz) at the workgroup's start and end
+    if (stamps && tid == 0) stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     PHASE(0);
     RT(0);
     HWID();
@@ -1601,6 +1604,10 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     PHASE(3);
     RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
+    if (stamps) {
+        __syncthreads();
+        if (tid == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // per (layer, out-channel) wave: scale = 2^(14 - floor(log2 max|w|)), split the scaled weights
@@ -1667,10 +1674,16 @@ static void launch_trunk(const float* x, int32_t n, const float* params, const u
                            dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
 }
 
+// workgroups of one h2 trunk launch (k_resnet_h2's grid)
+static int h2_grid(int bs, int filters, int n) {
+    if (bs == 6) return filters == 64 ? (n + 3) / 4 : n;
+    return filters == 64 ? (n + 1) / 2 : n;
+}
+
 template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
                             int32_t filters, int32_t blocks, float* work, float* logits,
-                            float* value, hipStream_t s) {
+                            float* value, hipStream_t s, uint64_t* stamps = nullptr) {
     const Layout L = make_layout(filters, blocks, BS);
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
@@ -1678,16 +1691,17 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
     if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
         if (filters == 64)
             hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), dim3((n + 3) / 4), dim3(256), 0, s,
-                               x, n, params, L, blob, blocks, work, logits, value);
+                               x, n, params, L, blob, blocks, work, logits, value, stamps);
         else
             hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), dim3(n), dim3(256), 0, s, x, n,
-                               params, L, blob, blocks, work, logits, value);
+                               params, L, blob, blocks, work, logits, value, stamps);
     } else if (filters == 64)
         hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), dim3((n + 1) / 2), dim3(256),
-                           RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value);
+                           RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value,
+                           stamps);
     else
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), dim3(n), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work, logits, value);
+                           params, L, blob, blocks, work, logits, value, stamps);
 }
 
 extern "C" {
@@ -1855,6 +1869,26 @@ int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* p
     hipStream_t s = (hipStream_t)stream;
     if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s);
     else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n) {
+    if (!board_ok(board) || (filters != 64 && filters != 128) || n < 0) return RVZ_EINVAL;
+    return h2_grid(board, filters, n);
+}
+
+int rvz_resnet_trunk_h2_stamped(int32_t board, const float* x, int32_t n, const float* params,
+                                const uint16_t* blob, int32_t filters, int32_t blocks,
+                                float* work, uint64_t* stamps, void* stream) {
+    if (!stamps || !x || !params || !blob || !work || n <= 0 || blocks < 0 || !board_ok(board) ||
+        (filters != 64 && filters != 128))
+        return RVZ_EINVAL;
+    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (board == 8)
+        launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, stamps);
+    else
+        launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, stamps);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 

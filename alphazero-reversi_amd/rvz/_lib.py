@@ -53,6 +53,13 @@ SIGNATURES = {
     "rvz_search_step": (C.c_int, [_P, _P, _P]),
     "rvz_search_submit": (C.c_int, [_P, _P, C.c_int32, _P]),
     "rvz_env_autoreset": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P, C.c_int32]),
+    "rvz_resnet_h2_grid": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32]),
+    "rvz_resnet_trunk_h2_stamped": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32,
+                                              C.c_int32, _P, _P, _P]),
+    "rvz_timer_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "rvz_timer_record": (C.c_int, [_P, C.c_int32, _P]),
+    "rvz_timer_elapsed": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_float)]),
+    "rvz_timer_destroy": (None, [_P]),
     "rvz_search_skip": (C.c_int, [_P]),
     "rvz_search_visits": (C.c_int, [_P, _P]),
     "rvz_act": (C.c_int, [_P, C.c_double, _P, C.c_int32, _P, _P]),
@@ -128,3 +135,34 @@ def ptr(t) -> int:
 
 def stream_handle(device=None) -> int:
     return torch.cuda.current_stream(device).cuda_stream
+
+
+class Timer:
+    """rvz_timer: stream-ordered HIP events without system fence (eager timing)."""
+
+    def __init__(self, n_events: int):
+        self.capacity = int(n_events)
+        h = C.c_void_p()
+        check(load().rvz_timer_create(self.capacity, C.byref(h)), None, "rvz_timer_create")
+        self.h = h
+        self.used = 0
+
+    def record(self, stream_handle) -> int:
+        if self.used >= self.capacity:
+            raise RvzError("timer full")
+        check(load().rvz_timer_record(self.h, self.used, stream_handle), None, "rvz_timer_record")
+        self.used += 1
+        return self.used - 1
+
+    def elapsed(self, i: int, j: int) -> float:
+        ms = C.c_float()
+        check(load().rvz_timer_elapsed(self.h, i, j, C.byref(ms)), None, "rvz_timer_elapsed")
+        return float(ms.value)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                load().rvz_timer_destroy(h)
+            except Exception:  # pragma: no cover - interpreter shutdown
+                pass

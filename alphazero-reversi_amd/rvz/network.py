@@ -172,6 +172,10 @@ class LeafEvaluator:
             kernel = "h2" if split_ok else "miopen"
         self.kernel = kernel
         self.use_resnet = kernel in ("h2", "split", "resnet")
+        # bench.py: (int64 [slots, grid, 2] stamp buffer, launches so far) to time every h2
+        # trunk launch from device wall-clock stamps, or None
+        self.trunk_stamps = None
+        self.trunk_events = None       # bench.py (eager): (rvz Timer, [(start, end) indices])
         self._outs = {}
         if self.use_resnet:
             from . import _lib
@@ -253,7 +257,38 @@ class LeafEvaluator:
                     torch.zeros(_lib.load().rvz_resnet_work_size(n), device=self.device))
             self._outs[n] = outs
         logits, value, work = outs
-        if self.kernel == "h2":
+        if self.kernel == "h2" and self.trunk_events is not None:
+            # eager timed form (bench.py): an event pair (rvz_timer, no system fence) around
+            # the trunk launch on its stream
+            lib, st = _lib.load(), _lib.stream_handle(x.device)
+            tm, pairs = self.trunk_events
+            a = tm.record(st)
+            _lib.check(lib.rvz_resnet_trunk_h2(
+                self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
+                self.filters, self.n_blocks, work.data_ptr(), st), None, "rvz_resnet_trunk_h2")
+            pairs.append((a, tm.record(st)))
+            _lib.check(lib.rvz_resnet_heads_fc(
+                self.board_size, work.data_ptr(), n, self.params.data_ptr(), self.filters,
+                self.n_blocks, logits.data_ptr(), value.data_ptr(), st), None,
+                "rvz_resnet_heads_fc")
+        elif self.kernel == "h2" and self.trunk_stamps is not None:
+            # instrumented form (bench.py): the two launches of rvz_resnet_fwd_h2, the trunk
+            # storing its workgroups' start / end wall clock in slot k of trunk_stamps
+            lib, st = _lib.load(), _lib.stream_handle(x.device)
+            buf, k = self.trunk_stamps
+            if k >= buf.shape[0] or buf.shape[1] != lib.rvz_resnet_h2_grid(
+                    self.board_size, self.filters, n):
+                raise _lib.RvzError("trunk stamp buffer too small")
+            _lib.check(lib.rvz_resnet_trunk_h2_stamped(
+                self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
+                self.filters, self.n_blocks, work.data_ptr(), buf[k].data_ptr(), st), None,
+                "rvz_resnet_trunk_h2_stamped")
+            self.trunk_stamps = (buf, k + 1)
+            _lib.check(lib.rvz_resnet_heads_fc(
+                self.board_size, work.data_ptr(), n, self.params.data_ptr(), self.filters,
+                self.n_blocks, logits.data_ptr(), value.data_ptr(), st), None,
+                "rvz_resnet_heads_fc")
+        elif self.kernel == "h2":
             _lib.check(_lib.load().rvz_resnet_fwd_h2(
                 self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
                 self.filters, self.n_blocks, work.data_ptr(), logits.data_ptr(),

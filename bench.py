@@ -117,8 +117,14 @@ def instrumented(run, eng, ev, plies):
         run.restart_finished(eng.get_state()[2])
 
     eng.timing_enable(True)
+    trunk_pairs, timer = None, None
+    if getattr(ev, "kernel", None) == "h2":
+        from rvz import _lib
+        trunk_pairs, timer = [], _lib.Timer(2 * plies * eng.n_batches)
+        ev.trunk_events = (timer, trunk_pairs)
     for _ in range(plies):
         one_ply()
+    ev.trunk_events = None
     t = eng.timing_read()
     eng.timing_enable(False)
     eng.stats_enable(True)
@@ -146,6 +152,8 @@ def instrumented(run, eng, ev, plies):
         b.record(stream)
         torch.cuda.synchronize(eng.device)
         ms["nn_trunk"] = a.elapsed_time(b) / 10
+    if trunk_pairs:   # the trunk launches of the timed plies, in their k_step -> trunk -> heads order
+        ms["nn_trunk_in_ply"] = sum(timer.elapsed(i, j) for i, j in trunk_pairs) / len(trunk_pairs)
     return ms, n, {"step": st, "act": act}
 
 
@@ -322,9 +330,22 @@ def main():
     eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
     run.start()
 
-    # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph
+    # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph with a
+    # HIP event pair around every trunk launch of lane 0 (read after the timed replays: the
+    # dominant kernel's duration inside the timed region)
+    graph_events = []
     warm = max(args.warmup, 0 if args.no_graph else 1)
     for i in range(warm):
+        if i == 0 and not args.no_graph and ev.kernel == "h2":
+            from rvz import _lib
+            run.ply()
+            grid = _lib.load().rvz_resnet_h2_grid(args.board, args.filters, eng.n_games)
+            stamps = torch.zeros(eng.n_batches, grid, 2, dtype=torch.int64, device=device)
+            ev.trunk_stamps = (stamps, 0)
+            run.capture()
+            graph_events = [stamps[:ev.trunk_stamps[1]]]
+            ev.trunk_stamps = None
+            continue
         run.ply()
         if i == 0 and not args.no_graph:
             run.capture()
@@ -340,6 +361,12 @@ def main():
     t1 = time.perf_counter()
     rdist.barrier()
     s1 = int(run.steps.item())
+    # the last timed replay's trunk launches (events hold their latest replay's timestamps)
+    trunk_live_ms = None
+    if graph_events:      # spans of the last replay's trunk launches, 100 MHz device clock
+        st_ = graph_events[0]
+        span = st_[:, :, 1].max(dim=1).values - st_[:, :, 0].min(dim=1).values
+        trunk_live_ms = float(span.double().mean().item()) * 1e-5
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
@@ -368,12 +395,24 @@ def main():
     split = "nn_trunk" in ms
     if split:   # roofline of the NN trunk kernel: executed 16-bit MFMA FLOPs per launch / duration
         mf = ev.mfma_flops_per_row() * lane_games
+        t_tr = ms["nn_trunk"]
         nn_roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
-                   "achieved": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12, 2),
+                   "achieved": round(mf / (t_tr * 1e-3) / 1e12, 2),
                    "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
-                   "frac": round(mf / (ms["nn_trunk"] * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
+                   "frac": round(mf / (t_tr * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
                    "traffic": pmc.get("nn_trunk", {}).get("hbm_bytes_per_launch"),
-                   "avg_ms_per_launch": round(ms["nn_trunk"], 4),
+                   "avg_ms_per_launch": round(t_tr, 4),
+                   "timing": "HIP events over 10 back-to-back launches on the bench batch, "
+                             "GPU busy throughout as in the timed graph replays (agrees with "
+                             "the rocprofv3 kernel average of the same command)",
+                   # cross-checks: (1) each trunk launch of the last timed graph replay, first
+                   # workgroup start to last workgroup end (s_memrealtime, 100 MHz; excludes the
+                   # dispatch ramp and completion that events and rocprof see); (2) fence-less
+                   # event pairs around each trunk launch in the eager instrumented plies (those
+                   # plies start from an idle GPU, so they read high: DVFS clock ramp)
+                   "live_span_ms": round(trunk_live_ms, 4) if trunk_live_ms else None,
+                   "avg_ms_in_eager_plies": (round(ms["nn_trunk_in_ply"], 4)
+                                             if "nn_trunk_in_ply" in ms else None),
                    "mfma_flops_per_launch": mf,
                    "fp32_equiv_tflops": round(nn_flops / (ms["nn_trunk"] * 1e-3) / 1e12, 2)}
     else:
@@ -384,7 +423,8 @@ def main():
     nn_roof["avg_ms_per_call"] = round(ms["nn"], 4)
     nn_roof["calls_per_ply"] = round(nn_per_ply, 2)
     search_ms_per_ply = kernels[dom]["avg_us"] * kernels[dom]["launches_per_ply"] / 1e3
-    nn_dominant = ms.get("nn_trunk", ms["nn"]) * nn_per_ply > search_ms_per_ply
+    nn_dominant = ms.get("nn_trunk", ms["nn"]) * nn_per_ply > \
+        search_ms_per_ply
 
     envb = env_bench(device, args.board) if rank == 0 else None
     cpu = None

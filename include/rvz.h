@@ -122,6 +122,15 @@ int rvz_act(rvz_engine *e, double temperature, const double *u, int32_t apply, i
             double *out_p);
 
 /* ---- introspection (tests / bench) -------------------------------------------------------- */
+/* Stream-ordered HIP event timer, events without system fence (the engine's own launch timing
+ * uses the same): record i / j around launches on a stream, rvz_timer_elapsed synchronises on j
+ * and returns the ms between them (host float). Not for stream capture. */
+typedef struct rvz_timer rvz_timer;
+int rvz_timer_create(int32_t n_events, rvz_timer **out);
+int rvz_timer_record(rvz_timer *t, int32_t i, void *hip_stream);
+int rvz_timer_elapsed(rvz_timer *t, int32_t i, int32_t j, float *ms /* host */);
+void rvz_timer_destroy(rvz_timer *t);
+
 /* Host copy of per-engine counters: [0] search batches issued, [1] kernel launches. */
 int rvz_counters(const rvz_engine *e, int64_t *out2 /* host */);
 /* Algorithmic-byte counters (bench roofline): while enabled, every search kernel adds the bytes
@@ -204,6 +213,15 @@ int rvz_resnet_fwd_h2(int32_t board, const float *x, int32_t n, const float *par
 int rvz_resnet_trunk_h2(int32_t board, const float *x, int32_t n, const float *params,
                         const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
                         void *hip_stream);
+/* Instrumented trunk (bench.py): as rvz_resnet_trunk_h2, and every workgroup w stores the
+ * device's 100 MHz wall clock (s_memrealtime) at its start and end in stamps[2w], stamps[2w+1]
+ * (uint64 [rvz_resnet_h2_grid(board, filters, n)][2]): max(end) - min(start) is the launch's
+ * span, readable after a replayed HIP graph (torch's HIP runtime refuses external event records
+ * in stream capture). */
+int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n);
+int rvz_resnet_trunk_h2_stamped(int32_t board, const float *x, int32_t n, const float *params,
+                                const uint16_t *blob, int32_t filters, int32_t blocks,
+                                float *work, uint64_t *stamps, void *hip_stream);
 
 #ifdef __cplusplus
 }

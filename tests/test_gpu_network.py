@@ -224,3 +224,33 @@ def test_h2_weight_blob():
     scaled_max = np.abs(ref).reshape(9, F, F).max(axis=(0, 2)) / isc[1]
     assert np.all((scaled_max >= 2 ** 14) & (scaled_max < 2 ** 15))
     assert prm.dtype == np.float32
+
+
+def test_h2_timing_forms_are_bit_identical():
+    """bench.py's instrumented forms of the h2 evaluator (trunk with per-workgroup wall-clock
+    stamps; fence-less event pair around the trunk) produce the same bits as the plain
+    rvz_resnet_fwd_h2, and the stamps are ordered (start <= end, nonzero)."""
+    import rvz
+    from rvz import _lib
+    net = _bn_net(2, 64, seed=8)
+    x = (torch.rand(96, 3, 8, 8, device="cuda") > 0.6).float()
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    l0, v0 = (t.clone() for t in ev(x))
+    grid = _lib.load().rvz_resnet_h2_grid(8, 64, 96)
+    assert grid > 0
+    stamps = torch.zeros(2, grid, 2, dtype=torch.int64, device="cuda")
+    ev.trunk_stamps = (stamps, 0)
+    l1, v1 = (t.clone() for t in ev(x))
+    assert ev.trunk_stamps[1] == 1
+    ev.trunk_stamps = None
+    ev.trunk_events = (_lib.Timer(2), [])
+    l2, v2 = (t.clone() for t in ev(x))
+    tm, pairs = ev.trunk_events
+    ev.trunk_events = None
+    torch.cuda.synchronize()
+    assert torch.equal(l0, l1) and torch.equal(v0, v1)
+    assert torch.equal(l0, l2) and torch.equal(v0, v2)
+    s = stamps[0].cpu()
+    assert bool((s > 0).all()) and bool((s[:, 1] >= s[:, 0]).all())
+    assert bool((stamps[1] == 0).all())
+    assert len(pairs) == 1 and 0.0 < tm.elapsed(*pairs[0]) < 1000.0

@@ -13,5 +13,5 @@ timeout -k 10 400 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.e
 rc=$?; echo "bench_rc=$rc"; [ $rc -ne 0 ] && exit $rc
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o bench \
-    -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
+    -- python bench.py --no-cpu-baseline > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
 rc=$?; echo "prof_rc=$rc"; exit $rc
