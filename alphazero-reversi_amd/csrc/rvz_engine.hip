@@ -87,6 +87,13 @@ struct View {  // kernel argument: device pointers + sizes
     int32_t* rng_pos;
     int32_t* err;
     unsigned long long* stats;  // [3][G] algorithmic bytes per game: k_step, k_act, k_expand_backup; or null
+    // compacted leaf batches (rvz_search_compact), or null: live[(e * NS + s) * PITCH] = live
+    // leaves of stripe s (games [s*STRIPE, (s+1)*STRIPE)) in batch e of the current search, at
+    // rows [s*STRIPE, s*STRIPE + count) of leaf_x; row_of[g] = game g's row
+    int32_t* live;   // [E][NS][PITCH]
+    int32_t* row_of;  // [G]
+    unsigned long long* live_total;  // running sum of the live counts (rows handed out)
+    int E, NS;
 };
 
 enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4 };
@@ -195,8 +202,9 @@ __device__ __forceinline__ ExpIn expand_load(const View& v, int g, int lane,
     x.V = v.leaf_legal[g];
     x.e = v.nexp[g];
     x.lm = v.leaf_meta[g];
-    x.val = value[g];
-    const float* row = policy + (size_t)g * NPOL;
+    const int r = v.live ? v.row_of[g] : g;
+    x.val = value[r];
+    const float* row = policy + (size_t)r * NPOL;
     x.prob = lane < NSQ ? row[lane] : 0.0f;
     x.xpass = row[NSQ];
     return x;
@@ -276,6 +284,7 @@ __device__ __forceinline__ void backup_visits_only(const View& v, int g, int lan
 // root / root_meta / root_n were loaded (or produced by the expand phase) by the caller.
 template <int BS, typename XT>
 __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int first, int bsz,
+                                             int eb,
                                              const GameS& root, uint32_t root_meta, int root_n,
                                              XT* __restrict__ leaf_x, int32_t* __restrict__ need,
                                              unsigned long long& ab) {
@@ -366,8 +375,18 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
             // queue `remaining` identical copies for the NN: encode get_canonical_state() planes
             copies = remaining;
             plen = depth + 1;
+            // compacted batch: the next free row of batch eb (one atomic per live game)
+            int r = g;
+            if (v.live) {   // striped counters: at most STRIPE contending waves per address
+                const int s = g / RVZ_LIVE_STRIPE;
+                if (lane == 0)
+                    r = s * RVZ_LIVE_STRIPE +
+                        atomicAdd(v.live + ((size_t)eb * v.NS + s) * RVZ_LIVE_PITCH, 1);
+                r = __shfl(r, 0);
+                if (lane == 0) v.row_of[g] = r;
+            }
             if (lane < NSQ) {
-                XT* row = leaf_x + (size_t)g * 3 * NSQ;
+                XT* row = leaf_x + (size_t)r * 3 * NSQ;
                 const uint64_t P = mine(sim), O = theirs(sim);
                 row[lane] = (XT)(float)((P >> lane) & 1ull);
                 row[NSQ + lane] = (XT)(float)((O >> lane) & 1ull);
@@ -396,7 +415,8 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
 template <int BS, typename XT>
 __global__ __launch_bounds__(256) void k_step(View v, int expand, const float* __restrict__ policy,
                                               int is_logits, const float* __restrict__ value,
-                                              int first, int bsz, XT* __restrict__ leaf_x,
+                                              int first, int bsz, int eb,
+                                              XT* __restrict__ leaf_x,
                                               int32_t* __restrict__ need) {
     const int lane = threadIdx.x & 63;
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
@@ -414,7 +434,7 @@ __global__ __launch_bounds__(256) void k_step(View v, int expand, const float* _
         const int rn = expand_backup_phase<BS>(v, g, lane, x, is_logits, &root_meta, ab_e);
         if (rn >= 0) root_n = rn;
     }
-    select_phase<BS, XT>(v, g, lane, first, bsz, root, root_meta, root_n, leaf_x, need, ab_s);
+    select_phase<BS, XT>(v, g, lane, first, bsz, eb, root, root_meta, root_n, leaf_x, need, ab_s);
     if (v.stats && lane == 0) v.stats[g] += ab_s + ab_e;  // per-game slot: no contention
 }
 
@@ -486,6 +506,14 @@ __global__ __launch_bounds__(256) void k_act(View v, int expand, const float* __
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = blockIdx.x * WPB + wid;
     if (g >= v.G) return;
+    // the search's leaf batches are all consumed (their NN calls precede this launch)
+    if (v.live && lane == 0) {
+        for (int i = g; i < v.E * v.NS; i += v.G) {
+            const int c = v.live[(size_t)i * RVZ_LIVE_PITCH];
+            if (c) atomicAdd(v.live_total, (unsigned long long)c);
+            v.live[(size_t)i * RVZ_LIVE_PITCH] = 0;
+        }
+    }
     unsigned long long ab = 0;
     if (expand == 1) {
         const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
@@ -717,6 +745,9 @@ struct rvz_engine {
     int BS, NSQ, NPOL, E, M;
     hipStream_t stream = nullptr;
     int next_batch = 0;  // batches issued in the current search
+    int32_t* live_buf = nullptr;    // rvz_search_compact: [E] live counts + [G] row map + total
+    unsigned long long* live_total = nullptr;
+    int live_dirty = 0;             // a k_step counted since the last k_act zeroed the counts
     int searching = 0;
     // a submitted batch whose expand + backup runs at the start of the next launch (k_step/k_act)
     int pending = 0;
@@ -824,6 +855,11 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     e->NPOL = e->NSQ + 1;
     e->E = E;
     e->M = 1 + E * e->NSQ;
+    e->v.E = E;
+    e->v.NS = (cfg->n_games + RVZ_LIVE_STRIPE - 1) / RVZ_LIVE_STRIPE;
+    e->v.live = nullptr;
+    e->v.row_of = nullptr;
+    e->v.live_total = nullptr;
     const int G = cfg->n_games;
     View& v = e->v;
     v.G = G;
@@ -1007,6 +1043,11 @@ int rvz_search_begin(rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
     e->next_batch = 0;
     e->searching = 1;
+    if (e->v.live && e->live_dirty) {   // an abandoned search left counts behind
+        RVZ_HIP(hipMemsetAsync(e->v.live, 0,
+                               sizeof(int32_t) * e->E * e->v.NS * RVZ_LIVE_PITCH, e->stream), e);
+        e->live_dirty = 0;
+    }
     e->pending = 0;  // an unconsumed submit of an abandoned search is dropped
     return RVZ_OK;
 }
@@ -1027,16 +1068,17 @@ int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
     timing_begin(e, 0);
     if (e->cfg.leaf_dtype == RVZ_LEAF_F32) {
         float* x = (float*)leaf_x;
-        if (e->BS == 8) hipLaunchKernelGGL((k_step<8, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
-        else hipLaunchKernelGGL((k_step<6, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
+        if (e->BS == 8) hipLaunchKernelGGL((k_step<8, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, e->next_batch, x, need);
+        else hipLaunchKernelGGL((k_step<6, float>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, e->next_batch, x, need);
     } else {
         __hip_bfloat16* x = (__hip_bfloat16*)leaf_x;
-        if (e->BS == 8) hipLaunchKernelGGL((k_step<8, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
-        else hipLaunchKernelGGL((k_step<6, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, x, need);
+        if (e->BS == 8) hipLaunchKernelGGL((k_step<8, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, e->next_batch, x, need);
+        else hipLaunchKernelGGL((k_step<6, __hip_bfloat16>), grid, block, 0, e->stream, e->v, ex, pol, lg, val, first, bsz, e->next_batch, x, need);
     }
     timing_end(e);
     e->pending = 0;
     e->next_batch += 1;
+    if (e->v.live) e->live_dirty = 1;
     e->counters[0] += 1;
     return launch_check(e, "k_step");
 }
@@ -1076,6 +1118,44 @@ int rvz_search_visits(rvz_engine* e, int32_t* out) {
     return launch_check(e, "k_visits");
 }
 
+int rvz_search_compact(rvz_engine* e, int32_t on) {
+    if (!e) return RVZ_EINVAL;
+    if (e->pending || (e->searching && e->next_batch > 0)) {
+        e->err = "rvz_search_compact inside a search";
+        return RVZ_EINVAL;
+    }
+    if (on && !e->live_buf) {
+        // [E] live counts, [G] row map, then the 8-byte running total
+        const size_t nlive = (size_t)e->E * e->v.NS * RVZ_LIVE_PITCH;
+        const size_t words = (nlive + e->v.G + 1) / 2 * 2 + 2;
+        e->live_buf = dalloc<int32_t>(e, words);
+        if (!e->live_buf) { e->err = "hipMalloc failed (live counts)"; return RVZ_ENOMEM; }
+        RVZ_HIP(hipMemsetAsync(e->live_buf, 0, sizeof(int32_t) * words, e->stream), e);
+        e->live_total = reinterpret_cast<unsigned long long*>(e->live_buf + words - 2);
+        e->live_dirty = 0;
+    }
+    e->v.live = on ? e->live_buf : nullptr;
+    e->v.row_of = on ? e->live_buf + (size_t)e->E * e->v.NS * RVZ_LIVE_PITCH : nullptr;
+    e->v.live_total = on ? e->live_total : nullptr;
+    return RVZ_OK;
+}
+
+int rvz_search_rows_total(rvz_engine* e, int64_t* out) {
+    if (!e || !out) return RVZ_EINVAL;
+    *out = 0;
+    if (!e->live_total) return RVZ_OK;
+    unsigned long long h = 0;
+    RVZ_HIP(hipMemcpyAsync(&h, e->live_total, sizeof(h), hipMemcpyDeviceToHost, e->stream), e);
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);
+    *out = (int64_t)h;
+    return RVZ_OK;
+}
+
+const int32_t* rvz_search_live_count(const rvz_engine* e) {
+    if (!e || !e->v.live || e->next_batch == 0) return nullptr;
+    return e->v.live + (size_t)(e->next_batch - 1) * e->v.NS * RVZ_LIVE_PITCH;
+}
+
 int rvz_search_skip(rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
     const int S = e->cfg.num_simulations, B = e->cfg.batch_size;
@@ -1098,6 +1178,7 @@ int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, i
     else hipLaunchKernelGGL(k_act<6>, grid, block, 0, e->stream, e->v, ex, e->pend_policy, e->pend_is_logits, e->pend_value, temperature, u, apply, out_idx, out_p);
     timing_end(e);
     e->pending = 0;
+    e->live_dirty = 0;
     if (apply) e->searching = 0;
     return launch_check(e, "k_act");
 }

@@ -333,11 +333,19 @@ __device__ __forceinline__ void head_fcs(const float* hpv, float* h1,
 #define RVZ_FCB 8
 #endif
 constexpr int FCB = RVZ_FCB;   // boards per workgroup (multiple of 4)
+static_assert(RVZ_LIVE_STRIPE % FCB == 0 && RVZ_LIVE_STRIPE % 16 == 0, "stripe granules");
+
+// a compacted leaf batch (include/rvz.h RVZ_LIVE_STRIPE): is the row past its stripe's live count?
+__device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int row) {
+    return n_live && row % RVZ_LIVE_STRIPE >= n_live[row / RVZ_LIVE_STRIPE * RVZ_LIVE_PITCH];
+}
 template <int BS>
 __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work, int n,
                                                   const float* __restrict__ prm, Layout L,
                                                   float* __restrict__ logits,
-                                                  float* __restrict__ value) {
+                                                  float* __restrict__ value,
+                                                  const int32_t* __restrict__ n_live) {
+    if (row_dead(n_live, (int)blockIdx.x * FCB)) return;   // the workgroup's rows are all dead
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1, ROW = 3 * CELLS;
     constexpr int VQ = CELLS / 4, PQ = PIN / 2 / 4;   // f32x4 per value row / policy half-row
     static_assert(CELLS % 4 == 0 && 2 * POUT <= 256, "thread map");
@@ -427,7 +435,9 @@ template <int BS>
 __global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ work, int n,
                                                     const float* __restrict__ prm, Layout L,
                                                     float* __restrict__ logits,
-                                                    float* __restrict__ value) {
+                                                    float* __restrict__ value,
+                                                    const int32_t* __restrict__ n_live) {
+    if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
     constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
     constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
@@ -1520,7 +1530,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, float* __restrict__ logits,
-                 float* __restrict__ value, uint64_t* __restrict__ stamps) {
+                 float* __restrict__ value, const int32_t* __restrict__ n_live,
+                 uint64_t* __restrict__ stamps) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
     using C = CfgH<F, G::NPIX>;
     using WT = WaveTilesH<F, CTW, PTW>;
@@ -1539,6 +1550,13 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     // optional device timestamps (bench.py: the launch's span inside a replayed HIP graph):
     // s_memrealtime (100 MHz) at the workgroup's start and end
     if (stamps && tid == 0) stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    // a compacted leaf batch (rvz_search_compact): dead boards are not evaluated, their rows are
+    // never read (uniform exit before the first barrier; NBOARD divides the stripe)
+    static_assert(RVZ_LIVE_STRIPE % NBOARD == 0, "stripe granule");
+    if (row_dead(n_live, g0)) {
+        if (stamps && tid == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
     PHASE(0);
     RT(0);
     HWID();
@@ -1683,7 +1701,8 @@ static int h2_grid(int bs, int filters, int n) {
 template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
                             int32_t filters, int32_t blocks, float* work, float* logits,
-                            float* value, hipStream_t s, uint64_t* stamps = nullptr) {
+                            float* value, hipStream_t s, const int32_t* n_live = nullptr,
+                            uint64_t* stamps = nullptr) {
     const Layout L = make_layout(filters, blocks, BS);
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
@@ -1691,17 +1710,17 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
     if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
         if (filters == 64)
             hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), dim3((n + 3) / 4), dim3(256), 0, s,
-                               x, n, params, L, blob, blocks, work, logits, value, stamps);
+                               x, n, params, L, blob, blocks, work, logits, value, n_live, stamps);
         else
             hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), dim3(n), dim3(256), 0, s, x, n,
-                               params, L, blob, blocks, work, logits, value, stamps);
+                               params, L, blob, blocks, work, logits, value, n_live, stamps);
     } else if (filters == 64)
         hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), dim3((n + 1) / 2), dim3(256),
                            RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value,
-                           stamps);
+                           n_live, stamps);
     else
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), dim3(n), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work, logits, value, stamps);
+                           params, L, blob, blocks, work, logits, value, n_live, stamps);
 }
 
 extern "C" {
@@ -1796,9 +1815,9 @@ int rvz_resnet_trunk_split(int32_t board, const float* x, int32_t n, const float
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
-int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float* params,
-                        int32_t filters, int32_t blocks, float* logits, float* value,
-                        void* stream) {
+int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const float* params,
+                           int32_t filters, int32_t blocks, float* logits, float* value,
+                           const int32_t* n_live, void* stream) {
     if (!work || !params || !logits || !value || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128))
         return RVZ_EINVAL;
@@ -1812,20 +1831,27 @@ int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float
         const dim3 grid((n + 15) / 16), block(256);
         if (board == 8)
             hipLaunchKernelGGL(k_heads_mfma<8>, grid, block, 0, (hipStream_t)stream, work, n,
-                               params, L, logits, value);
+                               params, L, logits, value, n_live);
         else
             hipLaunchKernelGGL(k_heads_mfma<6>, grid, block, 0, (hipStream_t)stream, work, n,
-                               params, L, logits, value);
+                               params, L, logits, value, n_live);
         return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
     }
     const dim3 grid((n + FCB - 1) / FCB), block(256);
     if (board == 8)
         hipLaunchKernelGGL(k_heads_fc<8>, grid, block, 0, (hipStream_t)stream, work, n, params,
-                           L, logits, value);
+                           L, logits, value, n_live);
     else
         hipLaunchKernelGGL(k_heads_fc<6>, grid, block, 0, (hipStream_t)stream, work, n, params,
-                           L, logits, value);
+                           L, logits, value, n_live);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float* params,
+                        int32_t filters, int32_t blocks, float* logits, float* value,
+                        void* stream) {
+    return rvz_resnet_heads_fc_ex(board, work, n, params, filters, blocks, logits, value, nullptr,
+                                  stream);
 }
 
 int rvz_resnet_fwd_split(int32_t board, const float* x, int32_t n, const float* params,
@@ -1858,18 +1884,29 @@ int rvz_resnet_h2_weights(const float* params, int32_t filters, int32_t blocks, 
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
-int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* params,
-                        const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
-                        void* stream) {
+int rvz_resnet_trunk_h2_ex(int32_t board, const float* x, int32_t n, const float* params,
+                           const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
+                           const int32_t* n_live, uint64_t* stamps, void* stream) {
     if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128))
         return RVZ_EINVAL;
     if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     hipStream_t s = (hipStream_t)stream;
-    if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s);
-    else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s);
+    if (board == 8)
+        launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, n_live,
+                           stamps);
+    else
+        launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, n_live,
+                           stamps);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
+int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* params,
+                        const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
+                        void* stream) {
+    return rvz_resnet_trunk_h2_ex(board, x, n, params, blob, filters, blocks, work, nullptr,
+                                  nullptr, stream);
 }
 
 int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n) {
@@ -1877,24 +1914,9 @@ int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n) {
     return h2_grid(board, filters, n);
 }
 
-int rvz_resnet_trunk_h2_stamped(int32_t board, const float* x, int32_t n, const float* params,
-                                const uint16_t* blob, int32_t filters, int32_t blocks,
-                                float* work, uint64_t* stamps, void* stream) {
-    if (!stamps || !x || !params || !blob || !work || n <= 0 || blocks < 0 || !board_ok(board) ||
-        (filters != 64 && filters != 128))
-        return RVZ_EINVAL;
-    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
-    hipStream_t s = (hipStream_t)stream;
-    if (board == 8)
-        launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, stamps);
-    else
-        launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, stamps);
-    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
-}
-
-int rvz_resnet_fwd_h2(int32_t board, const float* x, int32_t n, const float* params,
-                      const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
-                      float* logits, float* value, void* stream) {
+int rvz_resnet_fwd_h2_ex(int32_t board, const float* x, int32_t n, const float* params,
+                         const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
+                         float* logits, float* value, const int32_t* n_live, void* stream) {
     if (!logits || !value) return RVZ_EINVAL;
 #ifndef RVZ_H2_FC_IN
 #define RVZ_H2_FC_IN 0
@@ -1906,13 +1928,24 @@ int rvz_resnet_fwd_h2(int32_t board, const float* x, int32_t n, const float* par
         if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
         if (n == 0) return RVZ_OK;
         hipStream_t s = (hipStream_t)stream;
-        if (board == 8) launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, logits, value, s);
-        else launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, logits, value, s);
+        if (board == 8)
+            launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, logits, value, s, n_live);
+        else
+            launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, logits, value, s, n_live);
         return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
     }
-    const int rc = rvz_resnet_trunk_h2(board, x, n, params, blob, filters, blocks, work, stream);
+    const int rc = rvz_resnet_trunk_h2_ex(board, x, n, params, blob, filters, blocks, work, n_live,
+                                          nullptr, stream);
     if (rc != RVZ_OK) return rc;
-    return rvz_resnet_heads_fc(board, work, n, params, filters, blocks, logits, value, stream);
+    return rvz_resnet_heads_fc_ex(board, work, n, params, filters, blocks, logits, value, n_live,
+                                  stream);
+}
+
+int rvz_resnet_fwd_h2(int32_t board, const float* x, int32_t n, const float* params,
+                      const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
+                      float* logits, float* value, void* stream) {
+    return rvz_resnet_fwd_h2_ex(board, x, n, params, blob, filters, blocks, work, logits, value,
+                                nullptr, stream);
 }
 
 }  // extern "C"

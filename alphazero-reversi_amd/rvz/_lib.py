@@ -54,8 +54,15 @@ SIGNATURES = {
     "rvz_search_submit": (C.c_int, [_P, _P, C.c_int32, _P]),
     "rvz_env_autoreset": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P, C.c_int32]),
     "rvz_resnet_h2_grid": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32]),
-    "rvz_resnet_trunk_h2_stamped": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32,
-                                              C.c_int32, _P, _P, _P]),
+    "rvz_resnet_trunk_h2_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32,
+                                         C.c_int32, _P, _P, _P, _P]),
+    "rvz_resnet_heads_fc_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, C.c_int32, C.c_int32, _P,
+                                         _P, _P, _P]),
+    "rvz_resnet_fwd_h2_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32,
+                                       _P, _P, _P, _P, _P]),
+    "rvz_search_compact": (C.c_int, [_P, C.c_int32]),
+    "rvz_search_live_count": (C.c_void_p, [_P]),
+    "rvz_search_rows_total": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "rvz_timer_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
     "rvz_timer_record": (C.c_int, [_P, C.c_int32, _P]),
     "rvz_timer_elapsed": (C.c_int, [_P, C.c_int32, C.c_int32, C.POINTER(C.c_float)]),

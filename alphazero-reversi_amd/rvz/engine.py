@@ -36,7 +36,7 @@ def to_unsigned64(x: int) -> int:
 class Engine:
     def __init__(self, n_games: int, num_simulations: int = 800, batch_size: int = 64,
                  c_puct: float = 1.0, board_size: int = 8, device=None,
-                 leaf_dtype: torch.dtype = torch.float32):
+                 leaf_dtype: torch.dtype = torch.float32, compact_leaves: bool = False):
         if not torch.cuda.is_available():
             raise RvzError("rvz needs a HIP device (MI355X); there is no CPU fallback")
         self.lib = _lib.load()
@@ -70,6 +70,9 @@ class Engine:
         self.white = torch.zeros(G, dtype=torch.int64, device=dev)
         self.status = torch.zeros(G, 4, dtype=torch.int32, device=dev)
         self.n_batches = -(-num_simulations // batch_size)
+        self.compact_leaves = False
+        if compact_leaves:
+            self.compact(True)
 
     # ------------------------------------------------------------------ plumbing
     def __del__(self):
@@ -204,6 +207,27 @@ class Engine:
         rc = self._call("rvz_search_step", ptr(self.leaf_x), ptr(self.need))
         return rc != RVZ_DONE
 
+    def compact(self, on: bool = True):
+        """Compacted leaf batches (rvz_search_compact): the leaves that need an evaluation go to
+        rows [0, U) of leaf_x, U on the device (live_count()); an evaluator with
+        ``accepts_live_count`` evaluates only those rows (mcts.py:544-623 evaluates U leaves).
+        Same visits, p and moves as the uncompacted search."""
+        self._call("rvz_search_compact", int(bool(on)))
+        self.compact_leaves = bool(on)
+
+    def live_count(self) -> int:
+        """Device address of the int32 live-row count of the most recently issued batch."""
+        a = self.lib.rvz_search_live_count(self._h)
+        if not a:
+            raise RvzError("no live count: compaction off or no batch issued")
+        return int(a)
+
+    def rows_total(self) -> int:
+        """Live rows handed to the evaluator over all completed searches (compaction on)."""
+        out = C.c_int64()
+        self._call("rvz_search_rows_total", C.byref(out))
+        return int(out.value)
+
     def search_submit(self, policy: torch.Tensor, value: torch.Tensor, is_logits: bool):
         if policy.dtype != torch.float32 or value.dtype != torch.float32:
             raise RvzError("policy/value must be float32")
@@ -233,7 +257,10 @@ class Engine:
             if skip_last_eval and k == self.n_batches:
                 self.search_skip()
                 break
-            logits, value = evaluator(self.leaf_x)
+            if self.compact_leaves and getattr(evaluator, "accepts_live_count", False):
+                logits, value = evaluator(self.leaf_x, n_live=self.live_count())
+            else:
+                logits, value = evaluator(self.leaf_x)
             logits = logits.float().contiguous()
             value = value.float().contiguous()
             if fused_softmax:

@@ -246,7 +246,7 @@ class LeafEvaluator:
                    None, "rvz_nn_bias_act")
         return y
 
-    def _forward_resnet(self, x: torch.Tensor):
+    def _forward_resnet(self, x: torch.Tensor, n_live=None):
         from . import _lib
         n = x.shape[0]
         x = x.float().contiguous()
@@ -257,42 +257,39 @@ class LeafEvaluator:
                     torch.zeros(_lib.load().rvz_resnet_work_size(n), device=self.device))
             self._outs[n] = outs
         logits, value, work = outs
-        if self.kernel == "h2" and self.trunk_events is not None:
-            # eager timed form (bench.py): an event pair (rvz_timer, no system fence) around
-            # the trunk launch on its stream
+        live = int(n_live or 0)     # device address of the live row count, or 0 (all rows)
+        if self.kernel == "h2" and (self.trunk_events is not None or self.trunk_stamps is not None):
+            # instrumented forms (bench.py): the two launches of rvz_resnet_fwd_h2_ex with either
+            # an event pair (rvz_timer, no system fence) around the trunk launch (eager), or the
+            # trunk storing its workgroups' start / end wall clock in slot k of trunk_stamps
             lib, st = _lib.load(), _lib.stream_handle(x.device)
-            tm, pairs = self.trunk_events
-            a = tm.record(st)
-            _lib.check(lib.rvz_resnet_trunk_h2(
+            stamps, a = None, None
+            if self.trunk_events is not None:
+                tm, pairs = self.trunk_events
+                a = tm.record(st)
+            else:
+                buf, k = self.trunk_stamps
+                if k >= buf.shape[0] or buf.shape[1] != lib.rvz_resnet_h2_grid(
+                        self.board_size, self.filters, n):
+                    raise _lib.RvzError("trunk stamp buffer too small")
+                stamps = buf[k].data_ptr()
+                self.trunk_stamps = (buf, k + 1)
+            _lib.check(lib.rvz_resnet_trunk_h2_ex(
                 self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
-                self.filters, self.n_blocks, work.data_ptr(), st), None, "rvz_resnet_trunk_h2")
-            pairs.append((a, tm.record(st)))
-            _lib.check(lib.rvz_resnet_heads_fc(
+                self.filters, self.n_blocks, work.data_ptr(), live or None, stamps, st), None,
+                "rvz_resnet_trunk_h2_ex")
+            if a is not None:
+                pairs.append((a, tm.record(st)))
+            _lib.check(lib.rvz_resnet_heads_fc_ex(
                 self.board_size, work.data_ptr(), n, self.params.data_ptr(), self.filters,
-                self.n_blocks, logits.data_ptr(), value.data_ptr(), st), None,
-                "rvz_resnet_heads_fc")
-        elif self.kernel == "h2" and self.trunk_stamps is not None:
-            # instrumented form (bench.py): the two launches of rvz_resnet_fwd_h2, the trunk
-            # storing its workgroups' start / end wall clock in slot k of trunk_stamps
-            lib, st = _lib.load(), _lib.stream_handle(x.device)
-            buf, k = self.trunk_stamps
-            if k >= buf.shape[0] or buf.shape[1] != lib.rvz_resnet_h2_grid(
-                    self.board_size, self.filters, n):
-                raise _lib.RvzError("trunk stamp buffer too small")
-            _lib.check(lib.rvz_resnet_trunk_h2_stamped(
-                self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
-                self.filters, self.n_blocks, work.data_ptr(), buf[k].data_ptr(), st), None,
-                "rvz_resnet_trunk_h2_stamped")
-            self.trunk_stamps = (buf, k + 1)
-            _lib.check(lib.rvz_resnet_heads_fc(
-                self.board_size, work.data_ptr(), n, self.params.data_ptr(), self.filters,
-                self.n_blocks, logits.data_ptr(), value.data_ptr(), st), None,
-                "rvz_resnet_heads_fc")
+                self.n_blocks, logits.data_ptr(), value.data_ptr(), live or None, st), None,
+                "rvz_resnet_heads_fc_ex")
         elif self.kernel == "h2":
-            _lib.check(_lib.load().rvz_resnet_fwd_h2(
+            _lib.check(_lib.load().rvz_resnet_fwd_h2_ex(
                 self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
                 self.filters, self.n_blocks, work.data_ptr(), logits.data_ptr(),
-                value.data_ptr(), _lib.stream_handle(x.device)), None, "rvz_resnet_fwd_h2")
+                value.data_ptr(), live or None, _lib.stream_handle(x.device)), None,
+                "rvz_resnet_fwd_h2_ex")
         elif self.wsplit is not None:
             _lib.check(_lib.load().rvz_resnet_fwd_split(
                 self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
@@ -345,9 +342,17 @@ class LeafEvaluator:
         return terms * 2 * rows * f * (32 + 2 * self.n_blocks * 9 * f)
 
     @torch.no_grad()
-    def __call__(self, x: torch.Tensor):
+    @property
+    def accepts_live_count(self) -> bool:
+        """True when __call__ honours n_live (the h2 kernel): rows past the live count of a
+        compacted leaf batch are skipped."""
+        return self.kernel == "h2"
+
+    def __call__(self, x: torch.Tensor, n_live=None):
+        """n_live: device address (int) of an int32 count U (rvz_search_live_count): only rows
+        [0, U) need outputs. Honoured by the h2 kernel; the other forms evaluate every row."""
         if self.use_resnet:
-            return self._forward_resnet(x)
+            return self._forward_resnet(x, n_live)
         if self.fused:
             return self._forward_fused(x)
         cl = torch.channels_last

@@ -72,6 +72,10 @@ def parse():
                          "bit-identical games, one NN call fewer per move; off for the headline")
     ap.add_argument("--torch-bookkeeping", action="store_true",
                     help="per-ply counting / autoreset as torch ops instead of rvz_env_autoreset")
+    ap.add_argument("--no-compact", action="store_true",
+                    help="evaluate all n_games leaf rows of every batch instead of only the U "
+                         "live leaves (mcts.py:544-623 evaluates U; rows of games whose traversal "
+                         "ended on a terminal are dead)")
     ap.add_argument("--lanes", type=int, default=1,
                     help="independent game lanes per GPU, one stream each in one graph "
                          "(rvz.LaneRunner); the games are the same as with one lane")
@@ -309,7 +313,7 @@ def main():
 
     def make_eng(n):
         return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
-                          leaf_dtype=leaf_dtype)
+                          leaf_dtype=leaf_dtype, compact_leaves=not args.no_compact)
 
     first_game = rank * args.games          # global game index space: rank r owns a shard
     if args.lanes > 1:
@@ -351,6 +355,7 @@ def main():
             run.capture()
     torch.cuda.synchronize(device)
 
+    rows0 = sum(e.rows_total() for e in engines)
     rdist.barrier()
     torch.cuda.synchronize(device)
     s0 = int(run.steps.item())
@@ -361,6 +366,10 @@ def main():
     t1 = time.perf_counter()
     rdist.barrier()
     s1 = int(run.steps.item())
+    rows1 = sum(e.rows_total() for e in engines)
+    # leaf rows evaluated per NN call in the timed region (compaction on), else the full batch
+    nn_calls = args.steps * sum(e.n_batches for e in engines)
+    rows_per_call = (rows1 - rows0) / nn_calls if not args.no_compact else float(eng.n_games)
     # the last timed replay's trunk launches (events hold their latest replay's timestamps)
     trunk_live_ms = None
     if graph_events:      # spans of the last replay's trunk launches, 100 MHz device clock
@@ -402,9 +411,13 @@ def main():
                    "frac": round(mf / (t_tr * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
                    "traffic": pmc.get("nn_trunk", {}).get("hbm_bytes_per_launch"),
                    "avg_ms_per_launch": round(t_tr, 4),
-                   "timing": "HIP events over 10 back-to-back launches on the bench batch, "
-                             "GPU busy throughout as in the timed graph replays (agrees with "
-                             "the rocprofv3 kernel average of the same command)",
+                   "timing": "HIP events over 10 back-to-back launches on a full batch (every "
+                             "row live), GPU busy throughout as in the timed graph replays",
+                   # compacted batches: the timed region's launches evaluate this many live rows
+                   # on average (the endgame's terminal traversals need none), so the rocprofv3
+                   # average over a run sits below the full-batch duration by about that ratio
+                   "rows_per_launch": lane_games,
+                   "live_rows_per_launch_timed": round(rows_per_call, 1),
                    # cross-checks: (1) each trunk launch of the last timed graph replay, first
                    # workgroup start to last workgroup end (s_memrealtime, 100 MHz; excludes the
                    # dispatch ramp and completion that events and rocprof see); (2) fence-less

@@ -37,6 +37,13 @@ extern "C" {
 #define RVZ_LEAF_F32 0      /* leaf planes in float32, exactly game.get_canonical_state() */
 #define RVZ_LEAF_BF16 1     /* the same 0/1 planes as bfloat16 (exact) for a bf16 evaluator */
 
+/* Live-row counts of a compacted leaf batch (rvz_search_compact, the n_live argument of
+ * rvz_resnet_*_ex): the rows are handed out per stripe of RVZ_LIVE_STRIPE rows (game g draws
+ * from stripe g / RVZ_LIVE_STRIPE), one int32 counter per stripe, RVZ_LIVE_PITCH int32 apart;
+ * stripe s has its live rows at [s * RVZ_LIVE_STRIPE, s * RVZ_LIVE_STRIPE + n_live[s * PITCH]). */
+#define RVZ_LIVE_STRIPE 128
+#define RVZ_LIVE_PITCH 16
+
 typedef struct rvz_engine rvz_engine;
 
 typedef struct rvz_config {
@@ -111,6 +118,20 @@ int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, con
  * p and move of the evaluated search (tests/test_gpu_search.py::test_skip_last_eval_bit_exact).
  * An opt-in optimisation (one NN call fewer per move), not the reference's call sequence. */
 int rvz_search_skip(rvz_engine *e);
+/* Compacted leaf batches (on != 0; off by default): rvz_search_step writes the leaves that need an
+ * evaluation (need[g] > 0; mcts.py:544-623 evaluates exactly those) to the first rows of their
+ * game's stripe of RVZ_LIVE_STRIPE rows, in an unspecified order, and rvz_search_submit reads each
+ * game's policy / value from that game's row. The per-stripe counts stay on the device:
+ * rvz_search_live_count returns the address of the most recently issued batch's counts (layout
+ * above; stable for the engine's life per batch index of a search, so a captured graph may bake
+ * it in), for the n_live argument of rvz_resnet_*_ex. An evaluator that ignores them and
+ * evaluates all n_games rows gives the same search. Visits, p and moves are identical to the
+ * uncompacted search. */
+int rvz_search_compact(rvz_engine *e, int32_t on);
+const int32_t *rvz_search_live_count(const rvz_engine *e);
+/* Host int64: the live rows of every batch of every search completed by rvz_act since
+ * compaction was first enabled (0 if never enabled); synchronises the engine stream. */
+int rvz_search_rows_total(rvz_engine *e, int64_t *out /* host */);
 /* {move: child.visit_count} (mcts.py:406-407) as int32 [n_games, S*S+1] */
 int rvz_search_visits(rvz_engine *e, int32_t *out);
 /* get_action_probs' tail (mcts.py:656-692) + SelfPlay's make_move (self_play.py:98):
@@ -213,15 +234,25 @@ int rvz_resnet_fwd_h2(int32_t board, const float *x, int32_t n, const float *par
 int rvz_resnet_trunk_h2(int32_t board, const float *x, int32_t n, const float *params,
                         const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
                         void *hip_stream);
-/* Instrumented trunk (bench.py): as rvz_resnet_trunk_h2, and every workgroup w stores the
- * device's 100 MHz wall clock (s_memrealtime) at its start and end in stamps[2w], stamps[2w+1]
- * (uint64 [rvz_resnet_h2_grid(board, filters, n)][2]): max(end) - min(start) is the launch's
- * span, readable after a replayed HIP graph (torch's HIP runtime refuses external event records
- * in stream capture). */
+/* Extended forms. n_live (device int32 per-stripe counts as laid out at RVZ_LIVE_STRIPE, nullable):
+ * only the live rows of each stripe are evaluated (a compacted leaf batch, rvz_search_compact);
+ * workgroups whose boards are all dead exit at once and leave their rows of logits / value / work
+ * as they were. The row results do not
+ * depend on the row's position in the batch (tests/test_gpu_network.py). stamps (nullable,
+ * bench.py): every trunk workgroup w stores the device's 100 MHz wall clock (s_memrealtime) at its
+ * start and end in stamps[2w], stamps[2w+1] (uint64 [rvz_resnet_h2_grid(board, filters, n)][2]):
+ * max(end) - min(start) is the launch's span, readable after a replayed HIP graph (torch's HIP
+ * runtime refuses external event records in stream capture). */
 int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n);
-int rvz_resnet_trunk_h2_stamped(int32_t board, const float *x, int32_t n, const float *params,
-                                const uint16_t *blob, int32_t filters, int32_t blocks,
-                                float *work, uint64_t *stamps, void *hip_stream);
+int rvz_resnet_fwd_h2_ex(int32_t board, const float *x, int32_t n, const float *params,
+                         const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
+                         float *logits, float *value, const int32_t *n_live, void *hip_stream);
+int rvz_resnet_trunk_h2_ex(int32_t board, const float *x, int32_t n, const float *params,
+                           const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
+                           const int32_t *n_live, uint64_t *stamps, void *hip_stream);
+int rvz_resnet_heads_fc_ex(int32_t board, const float *work, int32_t n, const float *params,
+                           int32_t filters, int32_t blocks, float *logits, float *value,
+                           const int32_t *n_live, void *hip_stream);
 
 #ifdef __cplusplus
 }

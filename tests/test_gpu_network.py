@@ -254,3 +254,43 @@ def test_h2_timing_forms_are_bit_identical():
     assert bool((s > 0).all()) and bool((s[:, 1] >= s[:, 0]).all())
     assert bool((stamps[1] == 0).all())
     assert len(pairs) == 1 and 0.0 < tm.elapsed(*pairs[0]) < 1000.0
+
+
+@pytest.mark.parametrize("board,filters,n,lives", [(8, 64, 96, [37]), (8, 64, 96, [0]),
+                                                   (8, 64, 300, [37, 128, 5]),
+                                                   (6, 64, 300, [41, 0, 44]),
+                                                   (8, 128, 140, [17, 12])])
+def test_h2_live_rows(board, filters, n, lives):
+    """rvz_resnet_fwd_h2_ex with n_live (per-stripe live counts, include/rvz.h RVZ_LIVE_STRIPE):
+    the live rows of every stripe are bit-identical to the full evaluation, rows past the last
+    16-row heads group holding a live row of their stripe are left untouched, and a row's result
+    does not depend on its position in the batch (a permuted batch gives the permuted outputs),
+    which is what makes compacted leaf batches exact."""
+    import rvz
+    from rvz import _lib
+    lib = _lib.load()
+    S, PITCH = 128, 16          # RVZ_LIVE_STRIPE, RVZ_LIVE_PITCH
+    torch.manual_seed(board + filters)
+    net = rvz.AlphaZeroNetwork(board, 1, filters).cuda().eval()
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    x = (torch.rand(n, 3, board, board, device="cuda") > 0.6).float()
+    l0, v0 = (t.clone() for t in ev(x))
+    perm = torch.randperm(n, device="cuda")
+    lp, vp = ev(x[perm].contiguous())
+    assert torch.equal(lp, l0[perm]) and torch.equal(vp, v0[perm])
+    logits, value = ev(x)
+    logits.fill_(float("nan"))
+    value.fill_(float("nan"))
+    cnt = torch.zeros(len(lives) * PITCH, dtype=torch.int32, device="cuda")
+    cnt[::PITCH] = torch.tensor(lives, dtype=torch.int32)
+    assert lib.rvz_resnet_fwd_h2_ex(board, x.data_ptr(), n, ev.params.data_ptr(),
+                                    ev.wsplit.data_ptr(), filters, 1, ev._outs[n][2].data_ptr(),
+                                    logits.data_ptr(), value.data_ptr(), cnt.data_ptr(),
+                                    _lib.stream_handle()) == 0
+    torch.cuda.synchronize()
+    for s, live in enumerate(lives):
+        a, e = s * S, min(n, (s + 1) * S)
+        assert torch.equal(logits[a:a + live], l0[a:a + live]), s
+        assert torch.equal(value[a:a + live], v0[a:a + live]), s
+        tail = a + -(-live // 16) * 16
+        assert bool(torch.isnan(logits[tail:e]).all()) and bool(torch.isnan(value[tail:e]).all())

@@ -316,3 +316,44 @@ def test_fused_bookkeeping_matches_torch_path():
     for k, (x, y) in enumerate(zip(ta, tb)):
         for u, v in zip(x, y):
             assert torch.equal(u, v), k
+
+
+@pytest.mark.parametrize("live_aware", [True, False], ids=["n_live", "all_rows"])
+def test_compacted_leaves_play_the_same_games(live_aware):
+    """rvz_search_compact: the leaves that need an evaluation go to rows [0, U) of leaf_x and the
+    h2 evaluator evaluates only those (mcts.py:544-623 evaluates the U live leaves); an evaluator
+    that ignores the count evaluates every row. Either way the moves, p and boards equal the
+    uncompacted run's over whole games (the endgame's terminal traversals leave rows dead), and
+    the live-row total is what the need vectors say."""
+    import rvz
+    G, plies, sims = 96, 66, 128
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
+    runs, rows = [], None
+    for compact in (False, True):
+        eng = rvz.Engine(G, num_simulations=sims, batch_size=64, compact_leaves=compact)
+        ev = rvz.LeafEvaluator(net)
+        live_counts = []
+
+        def evaluator(x, n_live=None, ev=ev, eng=eng, live_counts=live_counts):
+            live_counts.append(int((eng.need > 0).sum()))
+            return ev(x, n_live=n_live)
+        evaluator.accepts_live_count = live_aware
+        run = rvz.SelfPlayRunner(eng, evaluator, autoreset=True, seed_base=11,
+                                 seed_stride=1000)
+        run.start()
+        trace = []
+        for _ in range(plies):
+            run.ply()
+            b, w, st = eng.get_state()
+            trace.append((eng.idx_buf.clone(), eng.p_buf.clone(), b.clone(), w.clone(),
+                          st.clone()))
+        runs.append((trace, int(run.games_done.item())))
+        if compact:
+            rows = (eng.rows_total(), sum(live_counts))
+    (ta, da), (tb, db) = runs
+    assert da == db and da >= G
+    for k, (x, y) in enumerate(zip(ta, tb)):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v), k
+    assert rows[0] == rows[1] and rows[1] < G * plies * 2
