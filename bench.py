@@ -37,10 +37,11 @@ MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense peaks, same source
 
 
 PRESETS = {   # BASELINE.json configs (index 0 is the reference's own single CPU game)
-    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8),
-    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8),
-    "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8),   # per GPU, x8 GPUs
-    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6),
+    # lanes: independent game lanes per GPU in one graph (same games; measured best per config)
+    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2),
+    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),
+    "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),  # per GPU, x8
+    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=1),
 }
 
 
@@ -76,7 +77,7 @@ def parse():
                     help="evaluate all n_games leaf rows of every batch instead of only the U "
                          "live leaves (mcts.py:544-623 evaluates U; rows of games whose traversal "
                          "ended on a terminal are dead)")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=None,
                     help="independent game lanes per GPU, one stream each in one graph "
                          "(rvz.LaneRunner); the games are the same as with one lane")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
@@ -391,7 +392,7 @@ def main():
     dom = max(("step", "act"),
               key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
     pmc = {}
-    if os.path.exists(args.pmc) and args.config == "c2" and eng.n_games == 4096:
+    if os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096:
         try:
             pmc = json.load(open(args.pmc))
         except Exception:
