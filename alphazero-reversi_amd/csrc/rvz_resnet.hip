@@ -1622,9 +1622,13 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     PHASE(3);
     RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
-    if (stamps) {
+    if (stamps) {   // end stamp; bits 56-63: the workgroup's live boards (bench.py's FLOPs)
+        const int rest = n_live ? n_live[g0 / RVZ_LIVE_STRIPE * RVZ_LIVE_PITCH] -
+                                      g0 % RVZ_LIVE_STRIPE
+                                : n_boards - g0;
+        const uint64_t nb = (uint64_t)(rest < NBOARD ? rest : NBOARD);
         __syncthreads();
-        if (tid == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() | (nb << 56);
     }
 }
 

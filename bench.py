@@ -372,11 +372,16 @@ def main():
     nn_calls = args.steps * sum(e.n_batches for e in engines)
     rows_per_call = (rows1 - rows0) / nn_calls if not args.no_compact else float(eng.n_games)
     # the last timed replay's trunk launches (events hold their latest replay's timestamps)
-    trunk_live_ms = None
+    # (lane 0; the stamps hold their latest replay's values; end stamp bits 56-63 = the
+    # workgroup's evaluated boards)
+    trunk_live = None
     if graph_events:      # spans of the last replay's trunk launches, 100 MHz device clock
         st_ = graph_events[0]
-        span = st_[:, :, 1].max(dim=1).values - st_[:, :, 0].min(dim=1).values
-        trunk_live_ms = float(span.double().mean().item()) * 1e-5
+        end = st_[:, :, 1] & ((1 << 56) - 1)
+        span = (end.max(dim=1).values - st_[:, :, 0].min(dim=1).values).double() * 1e-5
+        rows_k = (st_[:, :, 1] >> 56).sum(dim=1).double()
+        trunk_live = {"ms": float(span.mean().item()), "rows": float(rows_k.mean().item()),
+                      "rows_x_ms": float((rows_k / span).mean().item())}
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
@@ -404,31 +409,47 @@ def main():
     nn_per_ply = n["nn"] / max(1, args.instrument_plies)
     split = "nn_trunk" in ms
     if split:   # roofline of the NN trunk kernel: executed 16-bit MFMA FLOPs per launch / duration
-        mf = ev.mfma_flops_per_row() * lane_games
-        t_tr = ms["nn_trunk"]
+        fpr = ev.mfma_flops_per_row()
+        mf = fpr * lane_games
+        t_iso = ms["nn_trunk"]
+        peak = MFMA_PEAK_TFLOPS["bf16"]
+        iso = {"avg_ms_per_launch": round(t_iso, 4), "rows_per_launch": lane_games,
+               "achieved": round(mf / (t_iso * 1e-3) / 1e12, 2),
+               "frac": round(mf / (t_iso * 1e-3) / 1e12 / peak, 4),
+               "timing": "HIP events over 10 back-to-back launches of one full batch, no other "
+                         "lane running"}
+        if trunk_live:
+            # in the timed region: lane 0's trunk launches of the last timed graph replay, first
+            # workgroup start to last workgroup end (device s_memrealtime stamps, 100 MHz), and
+            # the rows those launches evaluated (from the stamps); with lanes > 1 the other
+            # lane's kernels share the chip during these launches, as in rocprofv3's view
+            ach = fpr * trunk_live["rows"] / (trunk_live["ms"] * 1e-3) / 1e12
+            t_tr, rows_tr = trunk_live["ms"], trunk_live["rows"]
+            timing = ("in the timed region: the trunk launches (lane 0) of the last timed graph "
+                      "replay, first workgroup start to last end (device s_memrealtime stamps)")
+        else:
+            ach, t_tr, rows_tr, timing = iso["achieved"], t_iso, lane_games, iso["timing"]
+        # the whole timed region: trunk MFMA FLOPs of every lane's evaluated rows / wall time
+        region = fpr * (rows1 - rows0 if not args.no_compact else nn_calls * lane_games) / \
+            (t1 - t0) / 1e12
         nn_roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
-                   "achieved": round(mf / (t_tr * 1e-3) / 1e12, 2),
-                   "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
-                   "frac": round(mf / (t_tr * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
+                   "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                   "frac": round(ach / peak, 4),
                    "traffic": pmc.get("nn_trunk", {}).get("hbm_bytes_per_launch"),
-                   "avg_ms_per_launch": round(t_tr, 4),
-                   "timing": "HIP events over 10 back-to-back launches on a full batch (every "
-                             "row live), GPU busy throughout as in the timed graph replays",
+                   "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": round(rows_tr, 1),
+                   "timing": timing,
+                   "isolated": iso,
                    # compacted batches: the timed region's launches evaluate this many live rows
-                   # on average (the endgame's terminal traversals need none), so the rocprofv3
-                   # average over a run sits below the full-batch duration by about that ratio
-                   "rows_per_launch": lane_games,
+                   # on average (the endgame's terminal traversals need none)
                    "live_rows_per_launch_timed": round(rows_per_call, 1),
-                   # cross-checks: (1) each trunk launch of the last timed graph replay, first
-                   # workgroup start to last workgroup end (s_memrealtime, 100 MHz; excludes the
-                   # dispatch ramp and completion that events and rocprof see); (2) fence-less
-                   # event pairs around each trunk launch in the eager instrumented plies (those
-                   # plies start from an idle GPU, so they read high: DVFS clock ramp)
-                   "live_span_ms": round(trunk_live_ms, 4) if trunk_live_ms else None,
+                   "timed_region_trunk_tflops": round(region, 2),
+                   "timed_region_trunk_frac": round(region / peak, 4),
+                   # fence-less event pairs around each trunk launch of the eager instrumented
+                   # plies (lane 0 alone)
                    "avg_ms_in_eager_plies": (round(ms["nn_trunk_in_ply"], 4)
                                              if "nn_trunk_in_ply" in ms else None),
-                   "mfma_flops_per_launch": mf,
-                   "fp32_equiv_tflops": round(nn_flops / (ms["nn_trunk"] * 1e-3) / 1e12, 2)}
+                   "mfma_flops_per_row": fpr,
+                   "fp32_equiv_tflops_isolated": round(nn_flops / (t_iso * 1e-3) / 1e12, 2)}
     else:
         nn_roof = {"kernel": "rvz_resnet_fwd_f32" if ev.use_resnet else "miopen",
                    "bound": "mfma", "achieved": round(nn_tflops, 2),
