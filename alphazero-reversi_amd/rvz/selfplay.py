@@ -157,14 +157,24 @@ class LaneRunner:
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)]
         self.temperature = float(temperature)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.lane_graphs = []         # capture(free_run=True): one graph per lane
 
     @property
     def steps(self) -> torch.Tensor:
+        self.join()
         return torch.stack([r.steps for r in self.runners]).sum()
 
     @property
     def games_done(self) -> torch.Tensor:
+        self.join()
         return torch.stack([r.games_done for r in self.runners]).sum()
+
+    def join(self):
+        """Make the current stream wait for every lane (free-running lanes are not joined per
+        ply)."""
+        main = torch.cuda.current_stream(self.runners[0].eng.device)
+        for s in self.streams:
+            main.wait_stream(s)
 
     def start(self):
         for r in self.runners:
@@ -179,17 +189,34 @@ class LaneRunner:
         for s in self.streams:
             main.wait_stream(s)
 
-    def capture(self):
+    def capture(self, free_run: bool = False):
+        """One graph holding every lane with a fork / join per ply, or (free_run) one graph per
+        lane replayed on the lane's own stream: the lanes then drift freely against each other
+        (no per-ply join bubble) and meet only at join() / a device synchronisation."""
         dev = self.runners[0].eng.device
         torch.cuda.synchronize(dev)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._body()
-        self.graph = g
+        if free_run:
+            self.lane_graphs = []
+            for r, s in zip(self.runners, self.streams):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    r._body()
+                self.lane_graphs.append(g)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body()
+            self.graph = g
         torch.cuda.synchronize(dev)
 
     def ply(self):
-        if self.graph is not None:
+        if self.lane_graphs:
+            main = torch.cuda.current_stream(self.runners[0].eng.device)
+            for g, s in zip(self.lane_graphs, self.streams):
+                s.wait_stream(main)
+                with torch.cuda.stream(s):
+                    g.replay()
+        elif self.graph is not None:
             self.graph.replay()
         else:
             self._body()

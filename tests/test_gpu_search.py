@@ -357,3 +357,31 @@ def test_compacted_leaves_play_the_same_games(live_aware):
         for u, v in zip(x, y):
             assert torch.equal(u, v), k
     assert rows[0] == rows[1] and rows[1] < G * plies * 2
+
+
+def test_free_running_lanes_play_the_same_games():
+    """LaneRunner.capture(free_run=True): one graph per lane on its own stream, no per-ply join;
+    after join() the boards, moves and counters equal the single-runner games."""
+    import rvz
+    G, plies, sims = 128, 12, 128
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
+    one = rvz.SelfPlayRunner(rvz.Engine(G, sims, 64, compact_leaves=True),
+                             rvz.LeafEvaluator(net), autoreset=True, seed_base=5)
+    lanes = rvz.LaneRunner(lambda n: rvz.Engine(n, sims, 64, compact_leaves=True),
+                           lambda: rvz.LeafEvaluator(net), G, 2, autoreset=True, seed_base=5)
+    one.start()
+    lanes.start()
+    one.ply()
+    lanes.ply()
+    one.capture()
+    lanes.capture(free_run=True)
+    for _ in range(plies):
+        one.ply()
+        lanes.ply()
+    assert int(lanes.steps.item()) == int(one.steps.item())
+    b1, w1, s1 = one.eng.get_state()
+    parts = [r.eng.get_state() for r in lanes.runners]
+    assert torch.equal(torch.cat([p[0] for p in parts]), b1)
+    assert torch.equal(torch.cat([p[1] for p in parts]), w1)
+    assert torch.equal(torch.cat([p[2] for p in parts]), s1)
