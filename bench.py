@@ -41,7 +41,7 @@ PRESETS = {   # BASELINE.json configs (index 0 is the reference's own single CPU
     "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2),
     "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),
     "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),  # per GPU, x8
-    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=1),
+    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2),
 }
 
 
