@@ -236,7 +236,7 @@ def cpu_baseline(args, net):
     torch.set_num_threads(cores)
     cpu_net = make_net(args, "cpu")
     cpu_net.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
-    G = 192                                   # ~11 s of C2 work on 16 host threads
+    G = 384                                   # ~10 s of C2 work on the GPU box's 16 host threads
     games = [O.new_game(args.board) for _ in range(G)]
     mts = [O.MT(args.seed + g) for g in range(G)]
     srch = O.Search(G, args.sims, args.batch, 1.0, bs=args.board)
