@@ -143,6 +143,11 @@ __device__ __forceinline__ int wave_argmax_first(float s, bool valid, int lane) 
     }
     return 63 - (int)(uint32_t)(k & 0xffffffffu);
 }
+// wave_argmax_first's order key of a non-NaN score (-0.0 ties +0.0)
+__device__ __forceinline__ uint32_t score_key(float s) {
+    const uint32_t b = __float_as_uint(s == 0.0f ? 0.0f : s);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
 
 // ---- backup (mcts.py:625-640): lane j updates path node plen-1-j; `copies` sequential adds ----
 // path_reg: lane i holds the i-th node of the path (root = lane 0). Returns the updated visit
@@ -314,6 +319,11 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
             int depth = 0, node = 0, parent_n = root_n;
             uint32_t m = root_meta;
             path_reg = 0;  // lane 0 holds the root
+            // per level d (in lane d): the chosen child's index, its turn for scoring, the best
+            // other child's score and index (-1: none) — the terminal fast path below
+            int fp_ci = 0, fp_b = -1, fp_turn = 0;
+            float fp_sb = 0.0f;
+            bool truncated = false;
             for (;;) {
                 const int nch = m_nchild(m);
                 if (m_term(m) || nch == 0) break;  // while node.expanded() and not terminal
@@ -342,6 +352,9 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                     }
                 }
                 const int ci = wave_argmax_first(score, lane < nch, lane);
+                const int bsib = wave_argmax_first(score, lane < nch && lane != ci, lane);
+                const float sbs = __shfl(score, bsib);
+                const int turn_c = 3 - m_turn(m);
                 if (v.stats) ab += 16ull * nch + 4ull * nch + 4ull * __popcll(__ballot(wrote));
                 node = base + ci;
                 m = (uint32_t)__shfl((int)cm, ci);
@@ -351,14 +364,68 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 if (depth >= PATH_CAP) {  // unreachable when ceil(sims/batch) <= 64 (checked)
                     if (lane == 0) atomicOr(v.err, ERR_PATH);
                     depth = PATH_CAP - 1;
+                    truncated = true;
                     break;
                 }
-                if (lane == depth) path_reg = node;
+                if (lane == depth) {
+                    path_reg = node;
+                    fp_ci = ci;
+                    fp_b = nch > 1 ? bsib : -1;
+                    fp_sb = sbs;
+                    fp_turn = turn_c;
+                }
             }
             if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
                 root_n = backup_path(nodes, path_reg, depth + 1, m_tv(m), 1, lane, true);
                 ab += 32ull * (depth + 1);
                 if (--remaining == 0) break;
+                if (truncated) continue;
+                // Fast path for the next traversals while they provably reach the same terminal.
+                // A backup invalidates only the path nodes' cached scores (mcts.py:639-640), so
+                // every other child on the path keeps the score this walk saw; the next walk
+                // takes the same child at level d iff the path child's fresh score (the reference
+                // formula on its backed-up N, W and its parent's N) beats the best other child
+                // under the first-index tie-break. Register copies of the path nodes replace the
+                // re-walk and its backup; the path is written back once (N, W, cache invalid)
+                // before the walk resumes at the first divergence or the batch ends.
+                const float tv = m_tv(m);
+                Node pn;
+                if (lane <= depth) pn = nodes[path_reg];
+                int fn = lane <= depth ? pn.n : 0;
+                float fw = lane <= depth ? pn.w : 0.0f;
+                const float fpr = lane <= depth ? pn.p : 0.0f;
+                int hits = 0;
+                for (;;) {
+                    const int par_n = __shfl_up(fn, 1);
+                    bool hold = true;
+                    if (lane >= 1 && lane <= depth && fp_b >= 0) {
+                        Node cn;
+                        cn.n = fn; cn.w = fw; cn.p = fpr; cn.c = 0.0f;
+                        const float sc = ucb_score(cn, (float)sqrt((double)par_n), fp_turn,
+                                                   v.cpuct);
+                        const uint32_t ks = score_key(sc), kb = score_key(fp_sb);
+                        hold = ks > kb || (ks == kb && fp_ci < fp_b);
+                    }
+                    if (__ballot(!hold) != 0ull) break;
+                    if (lane <= depth) {   // _backpropagate_path of the same terminal value
+                        fw = fw + (((depth - lane) & 1) ? -tv : tv);
+                        fn += 1;
+                    }
+                    ++hits;
+                    if (--remaining == 0) break;
+                }
+                if (hits) {
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    if (lane <= depth) {
+                        Node nd;
+                        nd.n = fn; nd.w = fw; nd.p = fpr; nd.c = __int_as_float(0x7fc00000);
+                        nodes[path_reg] = nd;
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                    root_n = __shfl(fn, 0);
+                }
+                ab += 32ull * (depth + 1);
+                if (remaining == 0) break;
                 continue;
             }
             // pass 1: valid moves of the leaf's simulated game
