@@ -324,6 +324,9 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
             int fp_ci = 0, fp_b = -1, fp_turn = 0;
             float fp_sb = 0.0f;
             bool truncated = false;
+            // the move of level d (lane d): replayed on `sim` only if the walk ends on a leaf
+            // that needs the position (a known terminal does not)
+            int fp_sq = 0;
             for (;;) {
                 const int nch = m_nchild(m);
                 if (m_term(m) || nch == 0) break;  // while node.expanded() and not terminal
@@ -359,7 +362,6 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 node = base + ci;
                 m = (uint32_t)__shfl((int)cm, ci);
                 parent_n = __shfl(c.n, ci);
-                make_move_wave<BS>(sim, m_sq(m), lane);
                 ++depth;
                 if (depth >= PATH_CAP) {  // unreachable when ceil(sims/batch) <= 64 (checked)
                     if (lane == 0) atomicOr(v.err, ERR_PATH);
@@ -369,6 +371,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 }
                 if (lane == depth) {
                     path_reg = node;
+                    fp_sq = m_sq(m);
                     fp_ci = ci;
                     fp_b = nch > 1 ? bsib : -1;
                     fp_sb = sbs;
@@ -428,6 +431,9 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 if (remaining == 0) break;
                 continue;
             }
+            // the leaf's position: the path's moves on the root's game (a truncated path, an
+            // error already flagged, replays its first PATH_CAP - 1 moves)
+            for (int d = 1; d <= depth; ++d) make_move_wave<BS>(sim, __shfl(fp_sq, d), lane);
             // pass 1: valid moves of the leaf's simulated game
             const uint64_t V = legal_wave<BS>(mine(sim), theirs(sim), lane);
             if (V == 0ull) {  // terminal, BLACK-absolute value from get_winner() (mcts.py:567-579)
