@@ -344,7 +344,10 @@ __global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work
                                                   const float* __restrict__ prm, Layout L,
                                                   float* __restrict__ logits,
                                                   float* __restrict__ value,
-                                                  const int32_t* __restrict__ n_live) {
+                                                  const int32_t* __restrict__ n_live,
+                                                  uint32_t* __restrict__ stamp_ctr) {
+    // bench.py: the trunk launch before this one is complete; advance its stamp ring
+    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
     if (row_dead(n_live, (int)blockIdx.x * FCB)) return;   // the workgroup's rows are all dead
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1, ROW = 3 * CELLS;
     constexpr int VQ = CELLS / 4, PQ = PIN / 2 / 4;   // f32x4 per value row / policy half-row
@@ -436,7 +439,10 @@ __global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ wo
                                                     const float* __restrict__ prm, Layout L,
                                                     float* __restrict__ logits,
                                                     float* __restrict__ value,
-                                                    const int32_t* __restrict__ n_live) {
+                                                    const int32_t* __restrict__ n_live,
+                                                    uint32_t* __restrict__ stamp_ctr) {
+    // bench.py: the trunk launch before this one is complete; advance its stamp ring
+    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
     if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
     constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
@@ -1531,7 +1537,8 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, float* __restrict__ logits,
                  float* __restrict__ value, const int32_t* __restrict__ n_live,
-                 uint64_t* __restrict__ stamps) {
+                 uint64_t* __restrict__ stamps, const uint32_t* __restrict__ stamp_ctr,
+                 int ring) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
     using C = CfgH<F, G::NPIX>;
     using WT = WaveTilesH<F, CTW, PTW>;
@@ -1549,12 +1556,21 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     bool ovf = false;
     // optional device timestamps (bench.py: the launch's span inside a replayed HIP graph):
     // s_memrealtime (100 MHz) at the workgroup's start and end
-    if (stamps && tid == 0) stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    // row of a ring of launches when stamp_ctr is given (advanced by the heads launch)
+    uint64_t t_start = 0;
+    if (stamps) {
+        t_start = __builtin_amdgcn_s_memrealtime();
+        const uint32_t slot = stamp_ctr ? *stamp_ctr % (uint32_t)ring : 0u;
+        stamps += ((size_t)slot * gridDim.x + blockIdx.x) * 2;
+    }
     // a compacted leaf batch (rvz_search_compact): dead boards are not evaluated, their rows are
     // never read (uniform exit before the first barrier; NBOARD divides the stripe)
     static_assert(RVZ_LIVE_STRIPE % NBOARD == 0, "stripe granule");
     if (row_dead(n_live, g0)) {
-        if (stamps && tid == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        if (stamps && tid == 0) {
+            stamps[0] = t_start;
+            stamps[1] = __builtin_amdgcn_s_memrealtime();
+        }
         return;
     }
     PHASE(0);
@@ -1628,7 +1644,10 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                                 : n_boards - g0;
         const uint64_t nb = (uint64_t)(rest < NBOARD ? rest : NBOARD);
         __syncthreads();
-        if (tid == 0) stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime() | (nb << 56);
+        if (tid == 0) {
+            stamps[0] = t_start;
+            stamps[1] = __builtin_amdgcn_s_memrealtime() | (nb << 56);
+        }
     }
 }
 
@@ -1706,7 +1725,8 @@ template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
                             int32_t filters, int32_t blocks, float* work, float* logits,
                             float* value, hipStream_t s, const int32_t* n_live = nullptr,
-                            uint64_t* stamps = nullptr) {
+                            uint64_t* stamps = nullptr, const uint32_t* stamp_ctr = nullptr,
+                            int ring = 1) {
     const Layout L = make_layout(filters, blocks, BS);
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
@@ -1714,17 +1734,17 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
     if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
         if (filters == 64)
             hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), dim3((n + 3) / 4), dim3(256), 0, s,
-                               x, n, params, L, blob, blocks, work, logits, value, n_live, stamps);
+                               x, n, params, L, blob, blocks, work, logits, value, n_live, stamps, stamp_ctr, ring);
         else
             hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), dim3(n), dim3(256), 0, s, x, n,
-                               params, L, blob, blocks, work, logits, value, n_live, stamps);
+                               params, L, blob, blocks, work, logits, value, n_live, stamps, stamp_ctr, ring);
     } else if (filters == 64)
         hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), dim3((n + 1) / 2), dim3(256),
                            RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value,
-                           n_live, stamps);
+                           n_live, stamps, stamp_ctr, ring);
     else
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), dim3(n), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work, logits, value, n_live, stamps);
+                           params, L, blob, blocks, work, logits, value, n_live, stamps, stamp_ctr, ring);
 }
 
 extern "C" {
@@ -1821,7 +1841,7 @@ int rvz_resnet_trunk_split(int32_t board, const float* x, int32_t n, const float
 
 int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const float* params,
                            int32_t filters, int32_t blocks, float* logits, float* value,
-                           const int32_t* n_live, void* stream) {
+                           const int32_t* n_live, uint32_t* stamp_ctr, void* stream) {
     if (!work || !params || !logits || !value || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128))
         return RVZ_EINVAL;
@@ -1835,19 +1855,19 @@ int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const fl
         const dim3 grid((n + 15) / 16), block(256);
         if (board == 8)
             hipLaunchKernelGGL(k_heads_mfma<8>, grid, block, 0, (hipStream_t)stream, work, n,
-                               params, L, logits, value, n_live);
+                               params, L, logits, value, n_live, stamp_ctr);
         else
             hipLaunchKernelGGL(k_heads_mfma<6>, grid, block, 0, (hipStream_t)stream, work, n,
-                               params, L, logits, value, n_live);
+                               params, L, logits, value, n_live, stamp_ctr);
         return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
     }
     const dim3 grid((n + FCB - 1) / FCB), block(256);
     if (board == 8)
         hipLaunchKernelGGL(k_heads_fc<8>, grid, block, 0, (hipStream_t)stream, work, n, params,
-                           L, logits, value, n_live);
+                           L, logits, value, n_live, stamp_ctr);
     else
         hipLaunchKernelGGL(k_heads_fc<6>, grid, block, 0, (hipStream_t)stream, work, n, params,
-                           L, logits, value, n_live);
+                           L, logits, value, n_live, stamp_ctr);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
@@ -1855,7 +1875,7 @@ int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float
                         int32_t filters, int32_t blocks, float* logits, float* value,
                         void* stream) {
     return rvz_resnet_heads_fc_ex(board, work, n, params, filters, blocks, logits, value, nullptr,
-                                  stream);
+                                  nullptr, stream);
 }
 
 int rvz_resnet_fwd_split(int32_t board, const float* x, int32_t n, const float* params,
@@ -1890,19 +1910,20 @@ int rvz_resnet_h2_weights(const float* params, int32_t filters, int32_t blocks, 
 
 int rvz_resnet_trunk_h2_ex(int32_t board, const float* x, int32_t n, const float* params,
                            const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
-                           const int32_t* n_live, uint64_t* stamps, void* stream) {
+                           const int32_t* n_live, uint64_t* stamps, const uint32_t* stamp_ctr,
+                           int32_t ring, void* stream) {
     if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
-        (filters != 64 && filters != 128))
+        (filters != 64 && filters != 128) || (stamp_ctr && (!stamps || ring <= 0)))
         return RVZ_EINVAL;
     if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     hipStream_t s = (hipStream_t)stream;
     if (board == 8)
         launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, n_live,
-                           stamps);
+                           stamps, stamp_ctr, ring > 0 ? ring : 1);
     else
         launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, n_live,
-                           stamps);
+                           stamps, stamp_ctr, ring > 0 ? ring : 1);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
@@ -1910,7 +1931,7 @@ int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* p
                         const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
                         void* stream) {
     return rvz_resnet_trunk_h2_ex(board, x, n, params, blob, filters, blocks, work, nullptr,
-                                  nullptr, stream);
+                                  nullptr, nullptr, 0, stream);
 }
 
 int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n) {
@@ -1939,10 +1960,10 @@ int rvz_resnet_fwd_h2_ex(int32_t board, const float* x, int32_t n, const float* 
         return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
     }
     const int rc = rvz_resnet_trunk_h2_ex(board, x, n, params, blob, filters, blocks, work, n_live,
-                                          nullptr, stream);
+                                          nullptr, nullptr, 0, stream);
     if (rc != RVZ_OK) return rc;
     return rvz_resnet_heads_fc_ex(board, work, n, params, filters, blocks, logits, value, n_live,
-                                  stream);
+                                  nullptr, stream);
 }
 
 int rvz_resnet_fwd_h2(int32_t board, const float* x, int32_t n, const float* params,

@@ -55,9 +55,9 @@ SIGNATURES = {
     "rvz_env_autoreset": (C.c_int, [_P, _P, _P, C.c_int64, _P, _P, C.c_int32]),
     "rvz_resnet_h2_grid": (C.c_int32, [C.c_int32, C.c_int32, C.c_int32]),
     "rvz_resnet_trunk_h2_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32,
-                                         C.c_int32, _P, _P, _P, _P]),
+                                         C.c_int32, _P, _P, _P, _P, C.c_int32, _P]),
     "rvz_resnet_heads_fc_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, C.c_int32, C.c_int32, _P,
-                                         _P, _P, _P]),
+                                         _P, _P, _P, _P]),
     "rvz_resnet_fwd_h2_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32,
                                        _P, _P, _P, _P, _P]),
     "rvz_search_compact": (C.c_int, [_P, C.c_int32]),

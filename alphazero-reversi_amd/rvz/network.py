@@ -172,8 +172,8 @@ class LeafEvaluator:
             kernel = "h2" if split_ok else "miopen"
         self.kernel = kernel
         self.use_resnet = kernel in ("h2", "split", "resnet")
-        # bench.py: (int64 [slots, grid, 2] stamp buffer, launches so far) to time every h2
-        # trunk launch from device wall-clock stamps, or None
+        # bench.py: (int64 [ring, grid, 2] stamp ring, int32 [1] device launch counter) to time
+        # every h2 trunk launch from device wall-clock stamps, or None
         self.trunk_stamps = None
         self.trunk_events = None       # bench.py (eager): (rvz Timer, [(start, end) indices])
         self._outs = {}
@@ -263,26 +263,24 @@ class LeafEvaluator:
             # an event pair (rvz_timer, no system fence) around the trunk launch (eager), or the
             # trunk storing its workgroups' start / end wall clock in slot k of trunk_stamps
             lib, st = _lib.load(), _lib.stream_handle(x.device)
-            stamps, a = None, None
+            stamps, ctr, ring, a = None, None, 0, None
             if self.trunk_events is not None:
                 tm, pairs = self.trunk_events
                 a = tm.record(st)
             else:
-                buf, k = self.trunk_stamps
-                if k >= buf.shape[0] or buf.shape[1] != lib.rvz_resnet_h2_grid(
-                        self.board_size, self.filters, n):
-                    raise _lib.RvzError("trunk stamp buffer too small")
-                stamps = buf[k].data_ptr()
-                self.trunk_stamps = (buf, k + 1)
+                buf, cnt = self.trunk_stamps       # int64 [ring, grid, 2], int32 [1] counter
+                if buf.shape[1] != lib.rvz_resnet_h2_grid(self.board_size, self.filters, n):
+                    raise _lib.RvzError("trunk stamp buffer does not match the batch")
+                stamps, ctr, ring = buf.data_ptr(), cnt.data_ptr(), buf.shape[0]
             _lib.check(lib.rvz_resnet_trunk_h2_ex(
                 self.board_size, x.data_ptr(), n, self.params.data_ptr(), self.wsplit.data_ptr(),
-                self.filters, self.n_blocks, work.data_ptr(), live or None, stamps, st), None,
-                "rvz_resnet_trunk_h2_ex")
+                self.filters, self.n_blocks, work.data_ptr(), live or None, stamps, ctr, ring,
+                st), None, "rvz_resnet_trunk_h2_ex")
             if a is not None:
                 pairs.append((a, tm.record(st)))
             _lib.check(lib.rvz_resnet_heads_fc_ex(
                 self.board_size, work.data_ptr(), n, self.params.data_ptr(), self.filters,
-                self.n_blocks, logits.data_ptr(), value.data_ptr(), live or None, st), None,
+                self.n_blocks, logits.data_ptr(), value.data_ptr(), live or None, ctr, st), None,
                 "rvz_resnet_heads_fc_ex")
         elif self.kernel == "h2":
             _lib.check(_lib.load().rvz_resnet_fwd_h2_ex(

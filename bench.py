@@ -338,9 +338,10 @@ def main():
     eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
     run.start()
 
-    # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph with a
-    # HIP event pair around every trunk launch of lane 0 (read after the timed replays: the
-    # dominant kernel's duration inside the timed region)
+    # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph with
+    # lane 0's trunk launches stamping a ring of per-workgroup device wall-clock stamps, one row
+    # per launch (the heads launch advances the ring's device counter): read after the timed
+    # replays, the dominant kernel's duration over every lane-0 launch of the timed region
     graph_events = []
     cap_kw = {"free_run": not args.joined_lanes} if args.lanes > 1 else {}
     warm = max(args.warmup, 0 if args.no_graph else 1)
@@ -349,10 +350,12 @@ def main():
             from rvz import _lib
             run.ply()
             grid = _lib.load().rvz_resnet_h2_grid(args.board, args.filters, eng.n_games)
-            stamps = torch.zeros(eng.n_batches, grid, 2, dtype=torch.int64, device=device)
-            ev.trunk_stamps = (stamps, 0)
+            ring = max(1, args.steps) * eng.n_batches
+            stamps = torch.zeros(ring, grid, 2, dtype=torch.int64, device=device)
+            ctr = torch.zeros(1, dtype=torch.int32, device=device)
+            ev.trunk_stamps = (stamps, ctr)
             run.capture(**cap_kw)
-            graph_events = [stamps[:ev.trunk_stamps[1]]]
+            graph_events = [stamps, ctr]
             ev.trunk_stamps = None
             continue
         run.ply()
@@ -361,6 +364,8 @@ def main():
     torch.cuda.synchronize(device)
 
     rows0 = sum(e.rows_total() for e in engines)
+    if graph_events:
+        graph_events[1].zero_()            # the ring starts with the timed region
     rdist.barrier()
     torch.cuda.synchronize(device)
     s0 = int(run.steps.item())
@@ -375,17 +380,17 @@ def main():
     # leaf rows evaluated per NN call in the timed region (compaction on), else the full batch
     nn_calls = args.steps * sum(e.n_batches for e in engines)
     rows_per_call = (rows1 - rows0) / nn_calls if not args.no_compact else float(eng.n_games)
-    # the last timed replay's trunk launches (events hold their latest replay's timestamps)
-    # (lane 0; the stamps hold their latest replay's values; end stamp bits 56-63 = the
-    # workgroup's evaluated boards)
+    # every lane-0 trunk launch of the timed region: first workgroup start to last workgroup end
+    # (100 MHz device clock; end stamp bits 56-63 = the workgroup's evaluated boards)
     trunk_live = None
-    if graph_events:      # spans of the last replay's trunk launches, 100 MHz device clock
-        st_ = graph_events[0]
+    if graph_events:
+        launches = int(graph_events[1].item())
+        st_ = graph_events[0][:min(launches, graph_events[0].shape[0])]
         end = st_[:, :, 1] & ((1 << 56) - 1)
         span = (end.max(dim=1).values - st_[:, :, 0].min(dim=1).values).double() * 1e-5
         rows_k = (st_[:, :, 1] >> 56).sum(dim=1).double()
         trunk_live = {"ms": float(span.mean().item()), "rows": float(rows_k.mean().item()),
-                      "rows_x_ms": float((rows_k / span).mean().item())}
+                      "launches": launches}
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
@@ -423,14 +428,14 @@ def main():
                "timing": "HIP events over 10 back-to-back launches of one full batch, no other "
                          "lane running"}
         if trunk_live:
-            # in the timed region: lane 0's trunk launches of the last timed graph replay, first
-            # workgroup start to last workgroup end (device s_memrealtime stamps, 100 MHz), and
-            # the rows those launches evaluated (from the stamps); with lanes > 1 the other
-            # lane's kernels share the chip during these launches, as in rocprofv3's view
+            # in the timed region: every trunk launch of lane 0, first workgroup start to last
+            # workgroup end (device s_memrealtime stamps, 100 MHz), and the rows those launches
+            # evaluated (from the stamps); with lanes > 1 the other lane's kernels share the chip
+            # during these launches, as in rocprofv3's view
             ach = fpr * trunk_live["rows"] / (trunk_live["ms"] * 1e-3) / 1e12
             t_tr, rows_tr = trunk_live["ms"], trunk_live["rows"]
-            timing = ("in the timed region: the trunk launches (lane 0) of the last timed graph "
-                      "replay, first workgroup start to last end (device s_memrealtime stamps)")
+            timing = (f"in the timed region: all {trunk_live['launches']} trunk launches of lane "
+                      "0, first workgroup start to last end (device s_memrealtime stamps)")
         else:
             ach, t_tr, rows_tr, timing = iso["achieved"], t_iso, lane_games, iso["timing"]
         # the whole timed region: trunk MFMA FLOPs of every lane's evaluated rows / wall time

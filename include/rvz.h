@@ -243,17 +243,21 @@ int rvz_resnet_trunk_h2(int32_t board, const float *x, int32_t n, const float *p
  * start and end in stamps[2w], stamps[2w+1] (uint64 [rvz_resnet_h2_grid(board, filters, n)][2];
  * bits 56-63 of the end stamp: the workgroup's evaluated boards, 0 for a dead workgroup):
  * max(end) - min(start) is the launch's span, readable after a replayed HIP graph (torch's HIP
- * runtime refuses external event records in stream capture). */
+ * runtime refuses external event records in stream capture). stamp_ctr (device uint32, nullable):
+ * stamps is a ring of `ring` such launch rows and the trunk writes row *stamp_ctr % ring; the
+ * heads launch given the same counter advances it by one (one thread, after the trunk is done),
+ * so a replayed graph stamps every launch. */
 int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n);
 int rvz_resnet_fwd_h2_ex(int32_t board, const float *x, int32_t n, const float *params,
                          const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
                          float *logits, float *value, const int32_t *n_live, void *hip_stream);
 int rvz_resnet_trunk_h2_ex(int32_t board, const float *x, int32_t n, const float *params,
                            const uint16_t *blob, int32_t filters, int32_t blocks, float *work,
-                           const int32_t *n_live, uint64_t *stamps, void *hip_stream);
+                           const int32_t *n_live, uint64_t *stamps, const uint32_t *stamp_ctr,
+                           int32_t ring, void *hip_stream);
 int rvz_resnet_heads_fc_ex(int32_t board, const float *work, int32_t n, const float *params,
                            int32_t filters, int32_t blocks, float *logits, float *value,
-                           const int32_t *n_live, void *hip_stream);
+                           const int32_t *n_live, uint32_t *stamp_ctr, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -239,10 +239,11 @@ def test_h2_timing_forms_are_bit_identical():
     grid = _lib.load().rvz_resnet_h2_grid(8, 64, 96)
     assert grid > 0
     stamps = torch.zeros(2, grid, 2, dtype=torch.int64, device="cuda")
-    ev.trunk_stamps = (stamps, 0)
+    ctr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ev.trunk_stamps = (stamps, ctr)
     l1, v1 = (t.clone() for t in ev(x))
-    assert ev.trunk_stamps[1] == 1
     ev.trunk_stamps = None
+    assert int(ctr.item()) == 1                      # the heads launch advanced the ring
     ev.trunk_events = (_lib.Timer(2), [])
     l2, v2 = (t.clone() for t in ev(x))
     tm, pairs = ev.trunk_events
