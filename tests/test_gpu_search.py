@@ -318,20 +318,23 @@ def test_fused_bookkeeping_matches_torch_path():
             assert torch.equal(u, v), k
 
 
-@pytest.mark.parametrize("live_aware", [True, False], ids=["n_live", "all_rows"])
-def test_compacted_leaves_play_the_same_games(live_aware):
+@pytest.mark.parametrize("board,live_aware,skip", [(8, True, False), (8, False, False),
+                                                   (6, True, False), (8, True, True)],
+                         ids=["8x8-n_live", "8x8-all_rows", "6x6-n_live", "8x8-n_live-skip"])
+def test_compacted_leaves_play_the_same_games(board, live_aware, skip):
     """rvz_search_compact: the leaves that need an evaluation go to rows [0, U) of leaf_x and the
     h2 evaluator evaluates only those (mcts.py:544-623 evaluates the U live leaves); an evaluator
     that ignores the count evaluates every row. Either way the moves, p and boards equal the
     uncompacted run's over whole games (the endgame's terminal traversals leave rows dead), and
     the live-row total is what the need vectors say."""
     import rvz
-    G, plies, sims = 96, 66, 128
+    G, plies, sims = (96, 66, 128) if board == 8 else (300, 40, 128)
     torch.manual_seed(0)
-    net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
+    net = rvz.AlphaZeroNetwork(board, 1, 64).cuda().eval()
     runs, rows = [], None
     for compact in (False, True):
-        eng = rvz.Engine(G, num_simulations=sims, batch_size=64, compact_leaves=compact)
+        eng = rvz.Engine(G, num_simulations=sims, batch_size=64, board_size=board,
+                         compact_leaves=compact)
         ev = rvz.LeafEvaluator(net)
         live_counts = []
 
@@ -340,7 +343,7 @@ def test_compacted_leaves_play_the_same_games(live_aware):
             return ev(x, n_live=n_live)
         evaluator.accepts_live_count = live_aware
         run = rvz.SelfPlayRunner(eng, evaluator, autoreset=True, seed_base=11,
-                                 seed_stride=1000)
+                                 seed_stride=1000, skip_last_eval=skip)
         run.start()
         trace = []
         for _ in range(plies):
@@ -356,7 +359,10 @@ def test_compacted_leaves_play_the_same_games(live_aware):
     for k, (x, y) in enumerate(zip(ta, tb)):
         for u, v in zip(x, y):
             assert torch.equal(u, v), k
-    assert rows[0] == rows[1] and rows[1] < G * plies * 2
+    # rows_total counts the skipped last batch's live rows too (queued, not evaluated)
+    assert rows[0] >= rows[1] and rows[0] < G * plies * 2
+    if not skip:
+        assert rows[0] == rows[1]
 
 
 def test_free_running_lanes_play_the_same_games():
