@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--joined-lanes", action="store_true",
                     help="one graph for all lanes with a fork / join per ply (default: one "
                          "graph per lane on its own stream, no per-ply join; +0.9%% at C2)")
+    ap.add_argument("--no-stamps", action="store_true",
+                    help="no device stamps in the timed graph (roofline from the isolated "
+                         "back-to-back launches)")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
@@ -346,7 +349,7 @@ def main():
     cap_kw = {"free_run": not args.joined_lanes} if args.lanes > 1 else {}
     warm = max(args.warmup, 0 if args.no_graph else 1)
     for i in range(warm):
-        if i == 0 and not args.no_graph and ev.kernel == "h2":
+        if i == 0 and not args.no_graph and ev.kernel == "h2" and not args.no_stamps:
             from rvz import _lib
             run.ply()
             grid = _lib.load().rvz_resnet_h2_grid(args.board, args.filters, eng.n_games)
