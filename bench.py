@@ -483,6 +483,14 @@ def main():
         search_roof = {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(ach, 2),
                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
                        "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic}
+        # the env + tree path as a whole — the search kernels' own algorithmic-byte
+        # counters per committed board-step (lane 0's instrumented plies) x the job's board-steps/s
+        bps = (bytes_["step"] + bytes_["act"]) / max(1, args.instrument_plies * eng.n_games)
+        path_roof = {"what": "env + tree (k_step + k_act algorithmic bytes per board-step, from "
+                             "the kernels' counters) x board-steps/s", "bound": "hbm",
+                     "bytes_per_board_step": round(bps, 1),
+                     "achieved": round(value * bps / 1e9, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(value * bps / 1e9 / HBM_PEAK_GBS, 5)}
         out = {
             "metric": f"self-play board-steps/sec @ {args.sims} sims/move, "
                       f"{args.board}x{args.board} Reversi",
@@ -513,6 +521,7 @@ def main():
             "search_roofline" if nn_dominant else "nn_roofline":
                 search_roof if nn_dominant else nn_roof,
             "kernels": {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()},
+            "path_roofline": path_roof,
             "env_roofline": envb,
             "cpu_baseline": cpu,
         }
