@@ -391,3 +391,42 @@ def test_free_running_lanes_play_the_same_games():
     assert torch.equal(torch.cat([p[0] for p in parts]), b1)
     assert torch.equal(torch.cat([p[1] for p in parts]), w1)
     assert torch.equal(torch.cat([p[2] for p in parts]), s1)
+
+
+def test_compact_api_errors():
+    """rvz_search_compact / rvz_search_live_count / the _ex stamp arguments fail loudly on misuse
+    (include/rvz.h): no live count before a batch or with compaction off, no toggling inside a
+    search, a stamp ring counter without a ring."""
+    import ctypes as C
+    import rvz
+    from rvz import _lib
+    lib = _lib.load()
+    eng = rvz.Engine(8, 128, 64)
+    with pytest.raises(rvz.RvzError):
+        eng.live_count()                                  # compaction off
+    eng.compact(True)
+    with pytest.raises(rvz.RvzError):
+        eng.live_count()                                  # no batch issued yet
+    eng.reset(list(range(8)))
+    eng.search_begin()
+    assert eng.search_step()
+    assert eng.live_count() != 0
+    with pytest.raises(rvz.RvzError):
+        eng.compact(False)                                # inside a search
+    torch.manual_seed(0)
+    ev = rvz.LeafEvaluator(rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval())
+    logits, value = ev(eng.leaf_x, n_live=eng.live_count())
+    eng.search_submit(logits, value, True)
+    while eng.search_step():
+        logits, value = ev(eng.leaf_x, n_live=eng.live_count())
+        eng.search_submit(logits, value, True)
+    eng.act(1.0, apply=True)
+    eng.check()
+    assert eng.rows_total() == 8 * 2                      # 2 batches, every game live
+    x = torch.zeros(8, 3, 8, 8, device="cuda")
+    work = torch.zeros(lib.rvz_resnet_work_size(8), device="cuda")
+    ctr = torch.zeros(1, dtype=torch.int32, device="cuda")
+    rc = lib.rvz_resnet_trunk_h2_ex(8, x.data_ptr(), 8, ev.params.data_ptr(),
+                                    ev.wsplit.data_ptr(), 64, 1, work.data_ptr(), None, None,
+                                    ctr.data_ptr(), 4, _lib.stream_handle())
+    assert rc == -22                                      # RVZ_EINVAL: counter without a ring
