@@ -242,9 +242,12 @@ class SelfPlay:
         self.games_played = 0
 
     def _play(self, num_games: int) -> List[Dict]:
+        # compacted leaf batches: only the live leaves are evaluated (as _process_batch does);
+        # the games are identical either way
         eng = Engine(num_games, self.args.get("num_simulations", 800),
                      self.args.get("batch_size", 64), self.args.get("c_puct", 1.0),
-                     device=self.device)
+                     device=self.device,
+                     compact_leaves=bool(self.args.get("compact_leaves", True)))
         run = SelfPlayRunner(eng, self.evaluator, self.args.get("temperature", 1.0),
                              fused_softmax=self.args.get("fused_softmax", True),
                              seed_base=self.seed + self.games_played, record=True)

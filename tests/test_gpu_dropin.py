@@ -97,6 +97,24 @@ def test_selfplay_dropin_records(tmp_path):
     assert data["action_probs"].shape[1] == 65 and len(data["states"]) == len(data["values"])
 
 
+def test_selfplay_dropin_compaction_is_exact(tmp_path):
+    """SelfPlay compacts its leaf batches by default (only live leaves reach the h2 evaluator);
+    the recorded games equal the uncompacted run's."""
+    import rvz
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 1, 64).cuda()
+    out = []
+    for compact in (True, False):
+        sp = rvz.SelfPlay(net, {"num_simulations": 128, "seed": 5, "compact_leaves": compact,
+                                "save_dir": str(tmp_path / str(compact))})
+        assert sp.evaluator.accepts_live_count
+        out.append(sp.generate_games(16))
+    for a, b in zip(*out):
+        assert a["winner"] == b["winner"] and len(a["states"]) == len(b["states"])
+        for pa, pb in zip(a["action_probs"], b["action_probs"]):
+            assert np.array_equal(pa, pb)
+
+
 def test_ddp_trainer_single_gpu_step_on_records():
     """DDPTrainer (no process group) consumes the engine's records directly and learns."""
     import rvz
