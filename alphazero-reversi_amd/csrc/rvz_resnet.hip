@@ -1392,26 +1392,30 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
                                         const f16x8 (&w)[CTW][2], int wave, int lane,
                                         EpiH<CTW, PTW>& er, bool& ovf) {
     const WaveTilesH<F, CTW, PTW> wt(wave, lane);
-    const int kq = 8 * (lane >> 4);
+    // K order h2_stem_slot: this lane group's taps 2g, 2g + 1 and (groups 0, 1) part of tap 8
+    const int kg = lane >> 4, ta = 2 * kg, tb = 2 * kg + 1;
+    const int oa = (ta / 3) * 10 + ta % 3, ob = (tb / 3) * 10 + tb % 3;
+    const float4* x4 = reinterpret_cast<const float4*>(xin);
     f16x8 a[PTW][2];
 #pragma unroll
     for (int u = 0; u < PTW; ++u) {
         using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
         const int px = wt.px[u], b = px / G::PPB, r = (px % G::PPB) / BS, cc = px % BS;
         const bool on = px < G::NVALID;               // padding rows: zero input
+        const int at = b * 100 + r * 10 + cc;         // tap 0 of this pixel in the padded image
+        const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 fa = on ? x4[at + oa] : z4;
+        const float4 fb = on ? x4[at + ob] : z4;
+        const float4 f8 = on && kg < 2 ? x4[at + 22] : z4;   // tap 8 = (+2 rows, +2 cols)
+        const float e6 = kg == 0 ? f8.x : f8.z, e7 = kg == 0 ? f8.y : 0.0f;
+        const f32x2 xs[4] = {f32x2{fa.x, fa.y}, f32x2{fa.z, fb.x}, f32x2{fb.y, fb.z},
+                             f32x2{e6, e7}};
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 h0, h1;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            f32x2 xv;
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int k = kq + 2 * i + e, t = k / 3, ch = k % 3;
-                xv[e] = k < 27 && on ? xin[(b * 100 + (r + t / 3) * 10 + (cc + t % 3)) * 4 + ch]
-                                     : 0.0f;
-            }
             uint32_t p0, p1;
-            split2x2(xv, p0, p1);
+            split2x2(xs[i], p0, p1);
             h0[i] = p0;
             h1[i] = p1;
         }
@@ -1653,6 +1657,17 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
 
 // per (layer, out-channel) wave: scale = 2^(14 - floor(log2 max|w|)), split the scaled weights
 // into the fragment layout, store 1/scale. Layer -1 (blockIdx.y == 0) is the stem.
+// The stem's K order (k_resnet_h2 stem_h2): slot k of lane group g = k / 8 holds tap 2g channels
+// 0-2 (s = k % 8 < 3), tap 2g + 1 channels 0-2 (s < 6); the ninth tap fills the spare slots:
+// group 0 s = 6, 7 -> tap 8 channels 0, 1; group 1 s = 6 -> tap 8 channel 2. Returns tap * 3 +
+// channel, or -1 for a zero slot. A lane then reads whole (tap) float4s of the padded input.
+__host__ __device__ constexpr int h2_stem_slot(int k) {
+    const int g = k / 8, s = k % 8;
+    return s < 3   ? (2 * g) * 3 + s
+           : s < 6 ? (2 * g + 1) * 3 + (s - 3)
+           : (g == 0 ? 24 + (s - 6) : (g == 1 && s == 6 ? 26 : -1));
+}
+
 __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm, Layout L, int F,
                                                    int NB, uint16_t* __restrict__ blob) {
     const int n = blockIdx.x, lyr = (int)blockIdx.y - 1, lane = threadIdx.x;
@@ -1680,8 +1695,8 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
     if (lyr < 0) {                             // stem: [part][ct][lane][8], k < 32
         uint16_t* o = blob + h2_stem_off(F, NB);
         if (lane < 32) {
-            const int k = lane, ln = (k / 8) * H2_TM + n % H2_TM;
-            const float w = k < 27 ? wget(k) * sc : 0.0f;
+            const int k = lane, ln = (k / 8) * H2_TM + n % H2_TM, ix = h2_stem_slot(k);
+            const float w = ix >= 0 ? wget(ix) * sc : 0.0f;
             const _Float16 h0 = (_Float16)w;
             const _Float16 h1 = (_Float16)(w - (float)h0);
             o[((0 * CT + ct) * 64 + ln) * 8 + k % 8] = __builtin_bit_cast(uint16_t, h0);
