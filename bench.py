@@ -387,13 +387,8 @@ def main():
     # (100 MHz device clock; end stamp bits 56-63 = the workgroup's evaluated boards)
     trunk_live = None
     if graph_events:
-        launches = int(graph_events[1].item())
-        st_ = graph_events[0][:min(launches, graph_events[0].shape[0])]
-        end = st_[:, :, 1] & ((1 << 56) - 1)
-        span = (end.max(dim=1).values - st_[:, :, 0].min(dim=1).values).double() * 1e-5
-        rows_k = (st_[:, :, 1] >> 56).sum(dim=1).double()
-        trunk_live = {"ms": float(span.mean().item()), "rows": float(rows_k.mean().item()),
-                      "launches": launches}
+        from rvz.measure import trunk_spans
+        trunk_live = trunk_spans(graph_events[0], int(graph_events[1].item()))
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)

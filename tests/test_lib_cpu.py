@@ -55,3 +55,28 @@ def test_engine_fails_loudly_without_gpu():
         rvz.Engine(4)
     with pytest.raises(RuntimeError):
         rvz.ReversiGame().get_valid_moves()
+
+
+def test_trunk_stamp_decoding():
+    """bench.py's in-situ trunk duration: per launch row, last workgroup end minus first start
+    (100 MHz ticks -> ms), evaluated boards from bits 56-63 of the end stamps; rows beyond the
+    counter are ignored, a wrapped ring keeps every row."""
+    import torch
+    from rvz.measure import trunk_spans
+    ring, grid = 4, 3
+    st = torch.zeros(ring, grid, 2, dtype=torch.int64)
+    # launch 0: starts 1000..1002, ends 31000..31002 -> span 30002 ticks; boards 2 + 2 + 1
+    # launch 1: starts 5000, ends 15000 -> span 10000 ticks; boards 2 + 0 + 0
+    for w in range(grid):
+        st[0, w, 0] = 1000 + w
+        st[0, w, 1] = (31000 + w) | ((2 if w < 2 else 1) << 56)
+        st[1, w, 0] = 5000
+        st[1, w, 1] = 15000 | ((2 if w == 0 else 0) << 56)
+    st[2:] = 999999                      # rows past the counter: ignored
+    r = trunk_spans(st, 2)
+    assert r["launches"] == 2
+    assert abs(r["ms"] - (30002 + 10000) / 2 / 1e5) < 1e-12
+    assert r["rows"] == (5 + 2) / 2
+    assert trunk_spans(st, 0) is None
+    full = trunk_spans(st[:2], 7)         # wrapped: both rows kept
+    assert full["launches"] == 7 and full["rows"] == 3.5
