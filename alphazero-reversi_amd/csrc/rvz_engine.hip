@@ -98,6 +98,18 @@ struct View {  // kernel argument: device pointers + sizes
 
 enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4 };
 
+// Walk counters of the select phase per game (instrumented builds only, -DRVZ_WALK_STATS:
+// tools/exp_walks.py): [0] walks from the root, [1] tree levels read, [2] known-terminal hits
+// backed up in memory, [3] hits taken by the register fast path, [4] new terminals found
+#ifdef RVZ_WALK_STATS
+constexpr int WALK_STATS_MAX = 1 << 16;
+__device__ unsigned int g_walk[WALK_STATS_MAX][5];
+#define WALK_STAT(i, k) \
+    if (lane == 0 && g < WALK_STATS_MAX) g_walk[g][i] += (k)
+#else
+#define WALK_STAT(i, k)
+#endif
+
 __device__ __forceinline__ GameS load_game(const View& v, int g) {
     GameS s;
     s.black = v.black[g];
@@ -315,6 +327,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
     if (!root.over) {
         int remaining = bsz;
         for (;;) {
+            WALK_STAT(0, 1);
             GameS sim = root;
             int depth = 0, node = 0, parent_n = root_n;
             uint32_t m = root_meta;
@@ -354,6 +367,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                         wrote = true;
                     }
                 }
+                WALK_STAT(1, 1);
                 const int ci = wave_argmax_first(score, lane < nch, lane);
                 const int bsib = wave_argmax_first(score, lane < nch && lane != ci, lane);
                 const float sbs = __shfl(score, bsib);
@@ -380,6 +394,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
             }
             if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
                 root_n = backup_path(nodes, path_reg, depth + 1, m_tv(m), 1, lane, true);
+                WALK_STAT(2, 1);
                 ab += 32ull * (depth + 1);
                 if (--remaining == 0) break;
                 if (truncated) continue;
@@ -415,6 +430,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                         fn += 1;
                     }
                     ++hits;
+                    WALK_STAT(3, 1);
                     if (--remaining == 0) break;
                 }
                 if (hits) {
@@ -440,6 +456,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 const int w = sim.over ? sim.winner : -1;
                 const uint32_t code = w == 1 ? 1u : (w == 2 ? 2u : 0u);
                 if (lane == 0) meta[node] = m | (1u << 8) | (code << 9);
+                WALK_STAT(4, 1);
                 backup_path(nodes, path_reg, depth + 1, w == 1 ? 1.0f : (w == 2 ? -1.0f : 0.0f),
                             remaining, lane, true);
                 ab += 4 + 32ull * (depth + 1);
@@ -1228,6 +1245,26 @@ const int32_t* rvz_search_live_count(const rvz_engine* e) {
     if (!e || !e->v.live || e->next_batch == 0) return nullptr;
     return e->v.live + (size_t)(e->next_batch - 1) * e->v.NS * RVZ_LIVE_PITCH;
 }
+
+#ifdef RVZ_WALK_STATS
+// host int64[10]: sums over games of the 5 walk counters, then their maxima; zeroes them
+int rvz_walk_stats(int32_t n_games, int64_t* out10) {
+    static std::vector<unsigned int> h;
+    const int n = n_games < WALK_STATS_MAX ? n_games : WALK_STATS_MAX;
+    h.assign((size_t)n * 5, 0u);
+    if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_walk), h.size() * 4) != hipSuccess)
+        return RVZ_EHIP;
+    for (int i = 0; i < 10; ++i) out10[i] = 0;
+    for (int gi = 0; gi < n; ++gi)
+        for (int i = 0; i < 5; ++i) {
+            out10[i] += h[(size_t)gi * 5 + i];
+            if ((int64_t)h[(size_t)gi * 5 + i] > out10[5 + i]) out10[5 + i] = h[(size_t)gi * 5 + i];
+        }
+    std::vector<unsigned int> z((size_t)WALK_STATS_MAX * 5, 0u);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_walk), z.data(), z.size() * 4) == hipSuccess
+               ? RVZ_OK : RVZ_EHIP;
+}
+#endif
 
 int rvz_search_skip(rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
