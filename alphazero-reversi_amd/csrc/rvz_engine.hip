@@ -106,8 +106,16 @@ constexpr int WALK_STATS_MAX = 1 << 16;
 __device__ unsigned int g_walk[WALK_STATS_MAX][5];
 #define WALK_STAT(i, k) \
     if (lane == 0 && g < WALK_STATS_MAX) g_walk[g][i] += (k)
+// shader-clock split of a game's k_step work: [0] expand phase, [1] walk levels, [2] memory
+// backups of known terminals, [3] register fast path, [4] leaf (position, legal moves, queue)
+__device__ unsigned long long g_wtime[WALK_STATS_MAX][5];
+#define WT_NOW(t) const uint64_t t = __builtin_amdgcn_s_memtime()
+#define WT_ADD(i, t0) \
+    if (lane == 0 && g < WALK_STATS_MAX) g_wtime[g][i] += __builtin_amdgcn_s_memtime() - (t0)
 #else
 #define WALK_STAT(i, k)
+#define WT_NOW(t)
+#define WT_ADD(i, t0)
 #endif
 
 __device__ __forceinline__ GameS load_game(const View& v, int g) {
@@ -140,25 +148,34 @@ __device__ __forceinline__ float wave_sum_f(float x) {
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
     return x;
 }
-// First index holding the maximum: Python's `if score > best_score` scan over the children dict
-// (mcts.py:423-428). NaN never wins (NaN > x is False); -0.0 ties +0.0.
-__device__ __forceinline__ int wave_argmax_first(float s, bool valid, int lane) {
-    const float z = (s == 0.0f) ? 0.0f : s;
-    const uint32_t b = __float_as_uint(z);
-    uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-    if (!valid || isnan(s)) key = 0u;
-    uint64_t k = ((uint64_t)key << 32) | (uint32_t)(63 - lane);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const uint64_t other = __shfl_xor(k, o);
-        k = other > k ? other : k;
-    }
-    return 63 - (int)(uint32_t)(k & 0xffffffffu);
-}
-// wave_argmax_first's order key of a non-NaN score (-0.0 ties +0.0)
+// Order key of a non-NaN score for an unsigned max (-0.0 ties +0.0).
 __device__ __forceinline__ uint32_t score_key(float s) {
     const uint32_t b = __float_as_uint(s == 0.0f ? 0.0f : s);
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+// Unsigned max over the wave on the DPP network (row shifts, then row broadcasts; lane 63 ends
+// with the total): no LDS crossbar traffic, unlike __shfl_xor (ds_bpermute).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+// First index holding the maximum: Python's `if score > best_score` scan over the children dict
+// (mcts.py:423-428). NaN never wins (NaN > x is False); -0.0 ties +0.0. The max key on the DPP
+// network, then the lowest lane holding it (all lanes invalid: lane 0).
+__device__ __forceinline__ int wave_argmax_first(float s, bool valid, int lane) {
+    const uint32_t key = (valid && !isnan(s)) ? score_key(s) : 0u;
+    const uint32_t m = wave_max_u32(key);
+    return __ffsll((unsigned long long)__ballot(key == m)) - 1;
+}
+// value of lane `src` (wave-uniform) to every lane
+__device__ __forceinline__ int lane_bcast(int x, int src) { return __builtin_amdgcn_readlane(x, src); }
+__device__ __forceinline__ float lane_bcast(float x, int src) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), src));
 }
 
 // ---- backup (mcts.py:625-640): lane j updates path node plen-1-j; `copies` sequential adds ----
@@ -328,6 +345,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
         int remaining = bsz;
         for (;;) {
             WALK_STAT(0, 1);
+            WT_NOW(tw0);
             GameS sim = root;
             int depth = 0, node = 0, parent_n = root_n;
             uint32_t m = root_meta;
@@ -370,12 +388,12 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 WALK_STAT(1, 1);
                 const int ci = wave_argmax_first(score, lane < nch, lane);
                 const int bsib = wave_argmax_first(score, lane < nch && lane != ci, lane);
-                const float sbs = __shfl(score, bsib);
+                const float sbs = lane_bcast(score, bsib);
                 const int turn_c = 3 - m_turn(m);
                 if (v.stats) ab += 16ull * nch + 4ull * nch + 4ull * __popcll(__ballot(wrote));
                 node = base + ci;
-                m = (uint32_t)__shfl((int)cm, ci);
-                parent_n = __shfl(c.n, ci);
+                m = (uint32_t)lane_bcast((int)cm, ci);
+                parent_n = lane_bcast(c.n, ci);
                 ++depth;
                 if (depth >= PATH_CAP) {  // unreachable when ceil(sims/batch) <= 64 (checked)
                     if (lane == 0) atomicOr(v.err, ERR_PATH);
@@ -392,9 +410,12 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                     fp_turn = turn_c;
                 }
             }
+            WT_ADD(1, tw0);
             if (m_term(m)) {  // known terminal: back up its value at once (mcts.py:364-366)
+                WT_NOW(tb0);
                 root_n = backup_path(nodes, path_reg, depth + 1, m_tv(m), 1, lane, true);
                 WALK_STAT(2, 1);
+                WT_ADD(2, tb0);
                 ab += 32ull * (depth + 1);
                 if (--remaining == 0) break;
                 if (truncated) continue;
@@ -406,6 +427,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 // under the first-index tie-break. Register copies of the path nodes replace the
                 // re-walk and its backup; the path is written back once (N, W, cache invalid)
                 // before the walk resumes at the first divergence or the batch ends.
+                WT_NOW(tf0);
                 const float tv = m_tv(m);
                 Node pn;
                 if (lane <= depth) pn = nodes[path_reg];
@@ -444,9 +466,11 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                     root_n = __shfl(fn, 0);
                 }
                 ab += 32ull * (depth + 1);
+                WT_ADD(3, tf0);
                 if (remaining == 0) break;
                 continue;
             }
+            WT_NOW(tl0);
             // the leaf's position: the path's moves on the root's game (a truncated path, an
             // error already flagged, replays its first PATH_CAP - 1 moves)
             for (int d = 1; d <= depth; ++d) make_move_wave<BS>(sim, __shfl(fp_sq, d), lane);
@@ -487,6 +511,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 v.leaf_legal[g] = V;
                 v.leaf_meta[g] = m;
             }
+            WT_ADD(4, tl0);
             ab += 3ull * NSQ * sizeof(XT) + 4ull * plen + 12;
             break;
         }
@@ -519,11 +544,13 @@ __global__ __launch_bounds__(256) void k_step(View v, int expand, const float* _
         root_n = v.nodes[(size_t)g * v.M].n;
     }
     unsigned long long ab_e = 0, ab_s = 0;
+    WT_NOW(te0);
     if (expand) {
         const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
         const int rn = expand_backup_phase<BS>(v, g, lane, x, is_logits, &root_meta, ab_e);
         if (rn >= 0) root_n = rn;
     }
+    WT_ADD(0, te0);
     select_phase<BS, XT>(v, g, lane, first, bsz, eb, root, root_meta, root_n, leaf_x, need, ab_s);
     if (v.stats && lane == 0) v.stats[g] += ab_s + ab_e;  // per-game slot: no contention
 }
@@ -1262,6 +1289,35 @@ int rvz_walk_stats(int32_t n_games, int64_t* out10) {
         }
     std::vector<unsigned int> z((size_t)WALK_STATS_MAX * 5, 0u);
     return hipMemcpyToSymbol(HIP_SYMBOL(g_walk), z.data(), z.size() * 4) == hipSuccess
+               ? RVZ_OK : RVZ_EHIP;
+}
+
+// host int64[11]: the 5 shader-clock categories of the game with the largest total, then the
+// means over games, then that game's index; zeroes them
+int rvz_walk_times(int32_t n_games, int64_t* out11) {
+    static std::vector<unsigned long long> h;
+    const int n = n_games < WALK_STATS_MAX ? n_games : WALK_STATS_MAX;
+    h.assign((size_t)n * 5, 0ull);
+    if (hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_wtime), h.size() * 8) != hipSuccess)
+        return RVZ_EHIP;
+    int best = 0;
+    unsigned long long bt = 0;
+    double mean[5] = {0, 0, 0, 0, 0};
+    for (int gi = 0; gi < n; ++gi) {
+        unsigned long long t = 0;
+        for (int i = 0; i < 5; ++i) {
+            t += h[(size_t)gi * 5 + i];
+            mean[i] += (double)h[(size_t)gi * 5 + i] / n;
+        }
+        if (t > bt) { bt = t; best = gi; }
+    }
+    for (int i = 0; i < 5; ++i) {
+        out11[i] = (int64_t)h[(size_t)best * 5 + i];
+        out11[5 + i] = (int64_t)mean[i];
+    }
+    out11[10] = best;
+    std::vector<unsigned long long> z((size_t)WALK_STATS_MAX * 5, 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_wtime), z.data(), z.size() * 8) == hipSuccess
                ? RVZ_OK : RVZ_EHIP;
 }
 #endif
