@@ -138,11 +138,6 @@ __device__ __forceinline__ int wave_sum_i(int x) {
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
     return x;
 }
-__device__ __forceinline__ float wave_max_f(float x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
-    return x;
-}
 __device__ __forceinline__ float wave_sum_f(float x) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
@@ -163,6 +158,17 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
+// fmaxf over the wave on the DPP network (order-independent: max is exact)
+__device__ __forceinline__ float wave_max_f(float x) {
+    const int ninf = (int)0xff800000u;   // -inf: the identity of the lanes a shift leaves empty
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x111, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x112, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x114, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x118, 0xf, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x142, 0xa, 0xf, false)));
+    x = fmaxf(x, __int_as_float(__builtin_amdgcn_update_dpp(ninf, __float_as_int(x), 0x143, 0xc, 0xf, false)));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
 }
 // First index holding the maximum: Python's `if score > best_score` scan over the children dict
 // (mcts.py:423-428). NaN never wins (NaN > x is False); -0.0 ties +0.0. The max key on the DPP
@@ -200,7 +206,7 @@ __device__ __forceinline__ int backup_path(Node* nodes, int path_reg, int plen, 
         n_after = nd.n;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    return __shfl(n_after, plen - 1);  // the lane that updated the root
+    return __builtin_amdgcn_readlane(n_after, plen - 1);  // the lane that updated the root
 }
 
 // UCB of an expanded child whose score is not cached (mcts.py:102-114); turn_c = child's turn.
@@ -254,7 +260,7 @@ __device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lan
     constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
     if (x.copies == 0) return -1;
     const int path_reg = lane < x.plen ? x.path_reg : 0;
-    const int leaf = __shfl(path_reg, x.plen - 1);
+    const int leaf = __builtin_amdgcn_readlane(path_reg, x.plen - 1);
     Node* nodes = v.nodes + (size_t)g * v.M;
     uint32_t* meta = v.meta + (size_t)g * v.M;
     float prob = x.prob;
@@ -463,7 +469,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                         nodes[path_reg] = nd;
                     }
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-                    root_n = __shfl(fn, 0);
+                    root_n = __builtin_amdgcn_readlane(fn, 0);
                 }
                 ab += 32ull * (depth + 1);
                 WT_ADD(3, tf0);
@@ -473,7 +479,8 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
             WT_NOW(tl0);
             // the leaf's position: the path's moves on the root's game (a truncated path, an
             // error already flagged, replays its first PATH_CAP - 1 moves)
-            for (int d = 1; d <= depth; ++d) make_move_wave<BS>(sim, __shfl(fp_sq, d), lane);
+            for (int d = 1; d <= depth; ++d)
+                make_move_wave<BS>(sim, __builtin_amdgcn_readlane(fp_sq, d), lane);
             // pass 1: valid moves of the leaf's simulated game
             const uint64_t V = legal_wave<BS>(mine(sim), theirs(sim), lane);
             if (V == 0ull) {  // terminal, BLACK-absolute value from get_winner() (mcts.py:567-579)
@@ -496,7 +503,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 if (lane == 0)
                     r = s * RVZ_LIVE_STRIPE +
                         atomicAdd(v.live + ((size_t)eb * v.NS + s) * RVZ_LIVE_PITCH, 1);
-                r = __shfl(r, 0);
+                r = __builtin_amdgcn_readlane(r, 0);
                 if (lane == 0) v.row_of[g] = r;
             }
             if (lane < NSQ) {
