@@ -191,11 +191,12 @@ __device__ __forceinline__ int backup_path(Node* nodes, int path_reg, int plen, 
                                            int copies, int lane, bool order_before) {
     // order this wave's earlier stores to path nodes (UCB caches) before the read-modify-write
     if (order_before) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    const int j = plen - 1 - lane;  // lane's path index counted from the root
-    const int nid = __shfl(path_reg, j < 0 ? 0 : j);
+    // lane d holds the path node at depth d (the root in lane 0): each lane updates its own node
+    const int nid = path_reg;
     int n_after = 0;
     if (lane < plen) {
-        const float sv = (lane & 1) ? -value : value;  // sign = +1 at the leaf, then alternates
+        // sign = +1 at the leaf (depth plen - 1), then alternates toward the root
+        const float sv = ((plen - 1 - lane) & 1) ? -value : value;
         Node nd = nodes[nid];
         float w = nd.w;
         for (int k = 0; k < copies; ++k) w = w + sv;
@@ -206,7 +207,7 @@ __device__ __forceinline__ int backup_path(Node* nodes, int path_reg, int plen, 
         n_after = nd.n;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    return __builtin_amdgcn_readlane(n_after, plen - 1);  // the lane that updated the root
+    return __builtin_amdgcn_readlane(n_after, 0);  // the root's lane
 }
 
 // UCB of an expanded child whose score is not cached (mcts.py:102-114); turn_c = child's turn.
@@ -312,9 +313,7 @@ __device__ __forceinline__ void backup_visits_only(const View& v, int g, int lan
     if (copies == 0) return;
     const int path_reg = lane < plen ? v.path[g * PATH_CAP + lane] : 0;
     Node* nodes = v.nodes + (size_t)g * v.M;
-    const int j = plen - 1 - lane;
-    const int nid = __shfl(path_reg, j < 0 ? 0 : j);
-    if (lane < plen) nodes[nid].n += copies;
+    if (lane < plen) nodes[path_reg].n += copies;   // lane d: the path node at depth d
     if (lane == 0) v.pend[g] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     if (v.stats) ab += 8ull + 4ull * plen + 8ull * plen;
