@@ -430,3 +430,39 @@ def test_compact_api_errors():
                                     ev.wsplit.data_ptr(), 64, 1, work.data_ptr(), None, None,
                                     ctr.data_ptr(), 4, _lib.stream_handle())
     assert rc == -22                                      # RVZ_EINVAL: counter without a ring
+
+
+def test_bench_configuration_at_full_size_plays_the_plain_games():
+    """The bench's C2 configuration at full size (4,096 games x 800 sims, 6x64 net; 2 free-running
+    lane graphs, compacted leaf batches) against the plain path (one runner, every row
+    evaluated, eager) over a whole game and its restarts: every ply's moves and the final boards,
+    statuses and ply counters are identical."""
+    import rvz
+    G, S, plies = 4096, 800, 64
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
+    lanes = rvz.LaneRunner(lambda n: rvz.Engine(n, S, 64, compact_leaves=True),
+                           lambda: rvz.LeafEvaluator(net), G, 2, autoreset=True, seed_base=42)
+    plain = rvz.SelfPlayRunner(rvz.Engine(G, S, 64), rvz.LeafEvaluator(net), autoreset=True,
+                               seed_base=42)
+    lanes.start()
+    plain.start()
+    lanes.ply()
+    plain.ply()
+    lanes.capture(free_run=True)
+    moves_l, moves_p = [], []
+    for _ in range(plies - 1):
+        lanes.ply()
+        plain.ply()
+        lanes.join()
+        moves_l.append(torch.cat([r.eng.idx_buf for r in lanes.runners]).clone())
+        moves_p.append(plain.eng.idx_buf.clone())
+    assert int(lanes.steps.item()) == int(plain.steps.item())
+    assert int(lanes.games_done.item()) == int(plain.games_done.item()) > 0
+    for k, (a, b) in enumerate(zip(moves_l, moves_p)):
+        assert torch.equal(a, b), k
+    parts = [r.eng.get_state() for r in lanes.runners]
+    b, w, st = plain.eng.get_state()
+    assert torch.equal(torch.cat([p[0] for p in parts]), b)
+    assert torch.equal(torch.cat([p[1] for p in parts]), w)
+    assert torch.equal(torch.cat([p[2] for p in parts]), st)
