@@ -22,8 +22,8 @@
 //    balanced tree), so u = c*P*sqrt(Np) / (1 + N).
 //  * value_sum is float32 (NumPy>=2 promotion of the np.float32 NN value); terminal values are
 //    small integers, exact in float32, so one float32 accumulator reproduces the Python mix.
-//  * sqrt(Np) is taken from a host-built table of (float)sqrt((double)n) (math.sqrt then the
-//    float32 cast), so no device sqrt rounding enters the scores.
+//  * sqrt(Np) is (float)sqrt((double)n) computed on the device: gfx950's f64 sqrt is correctly
+//    rounded (tests/test_gpu_numerics.py), so it equals math.sqrt then the float32 cast.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -96,7 +96,9 @@ struct View {  // kernel argument: device pointers + sizes
     int E, NS;
 };
 
-enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4 };
+// ERR_NN: an evaluator handed the expand a non-finite value or probability (an overflowed or
+// broken leaf evaluator must not feed the tree silently; the reference would play on with NaN)
+enum : int32_t { ERR_RNG = 1, ERR_POOL = 2, ERR_PATH = 4, ERR_NN = 8 };
 
 // Walk counters of the select phase per game (instrumented builds only, -DRVZ_WALK_STATS:
 // tools/exp_walks.py): [0] walks from the root, [1] tree levels read, [2] known-terminal hits
@@ -270,6 +272,11 @@ __device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lan
         const float ex = lane < NSQ ? expf(prob - mx) : 0.0f;
         const float denom = wave_sum_f(ex) + expf(x.xpass - mx);
         prob = ex / denom;
+    }
+    {   // non-finite NN output (any of the 65 probabilities or the value): device error word
+        const bool bad = !__builtin_isfinite(x.val) || !__builtin_isfinite(x.xpass) ||
+                         (lane < NSQ && !__builtin_isfinite(prob));
+        if (__builtin_amdgcn_ballot_w64(bad) && lane == 0) atomicOr(v.err, ERR_NN);
     }
     const int base = 1 + x.e * NSQ;
     if (base + NSQ > v.M) {
@@ -1063,7 +1070,8 @@ int rvz_check(rvz_engine* e, int32_t* host_err) {
     if (h) {
         RVZ_HIP(hipMemsetAsync(e->v.err, 0, sizeof(int32_t), e->stream), e);
         e->err = "device error word " + std::to_string(h) +
-                 " (1: rng stream exhausted, 2: node pool, 4: path depth)";
+                 " (1: rng stream exhausted, 2: node pool, 4: path depth, 8: non-finite NN "
+                 "value or probability)";
         return RVZ_EDEVICE;
     }
     return RVZ_OK;

@@ -93,10 +93,19 @@ class Engine:
         return check(getattr(self.lib, name)(self._h, *args), self._h, name)
 
     def check(self) -> None:
-        """Synchronise and raise if a kernel set the device error word."""
+        """Synchronise and raise RvzError if a kernel set the device error word (node pool, path
+        depth, RNG stream, non-finite NN output) or an evaluator this engine's searches used
+        reports an activation overflow (LeafEvaluator.overflowed: h2's sticky device word).
+        Both are accumulated on the device and read only here, so graph replays stay sync-free."""
         self._stream()
         err = C.c_int32(0)
         self._call("rvz_check", C.byref(err))
+        for ev in getattr(self, "_evaluators", ()):
+            of = getattr(ev, "overflowed", None)
+            if of is not None and of():
+                raise RvzError(f"leaf evaluator ({getattr(ev, 'kernel', type(ev).__name__)}) "
+                               "overflowed its f16 activation range (|x| >= 65520): the NN "
+                               "outputs of the searches are not valid")
 
     def counters(self) -> Tuple[int, int]:
         out = (C.c_int64 * 2)()
@@ -245,11 +254,15 @@ class Engine:
 
     def search(self, evaluator: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]],
                fused_softmax: bool = True, skip_last_eval: bool = False):
-        """MCTS.search for every live game. evaluator(leaf_x) -> (logits, value).
+        """MCTS.search for every live game. evaluator(leaf_x) -> (logits, value), or
+        (probabilities, value) when the evaluator has ``outputs_probs = True``.
 
         fused_softmax=False applies torch's F.softmax (the reference's mcts.py:596) before the
         expand kernel instead of the kernel's fused softmax. skip_last_eval=True does not
         evaluate the last batch (rvz_search_skip; bit-identical visits, one NN call fewer)."""
+        evs = self.__dict__.setdefault("_evaluators", [])
+        if not any(e is evaluator for e in evs):
+            evs.append(evaluator)             # read by check()
         self.search_begin()
         k = 0
         while self.search_step():
@@ -263,7 +276,10 @@ class Engine:
                 logits, value = evaluator(self.leaf_x)
             logits = logits.float().contiguous()
             value = value.float().contiguous()
-            if fused_softmax:
+            if getattr(evaluator, "outputs_probs", False):
+                # the evaluator hands over softmaxed rows (e.g. recorded reference outputs)
+                self.search_submit(logits, value, False)
+            elif fused_softmax:
                 self.search_submit(logits, value, True)
             else:
                 self.search_submit(torch.softmax(logits, dim=1).contiguous(), value, False)

@@ -339,7 +339,6 @@ class LeafEvaluator:
         terms = 3 if self.kernel == "h2" else 6
         return terms * 2 * rows * f * (32 + 2 * self.n_blocks * 9 * f)
 
-    @torch.no_grad()
     @property
     def accepts_live_count(self) -> bool:
         """True when __call__ honours n_live (the h2 kernel): rows past the live count of a

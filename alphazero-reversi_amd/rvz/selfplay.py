@@ -74,6 +74,11 @@ class SelfPlayRunner:
         self.eng.reset(self.seeds)
         self.ply_index = 0
 
+    def check(self):
+        """Synchronise; raise RvzError on a device error word or an evaluator overflow
+        (Engine.check)."""
+        self.eng.check()
+
     # one ply for every game; graph-capturable (no host sync)
     def _body(self):
         eng = self.eng
@@ -180,6 +185,11 @@ class LaneRunner:
         for r in self.runners:
             r.start()
 
+    def check(self):
+        self.join()
+        for r in self.runners:
+            r.check()
+
     def _body(self):
         main = torch.cuda.current_stream(self.runners[0].eng.device)
         for r, s in zip(self.runners, self.streams):
@@ -225,7 +235,11 @@ class LaneRunner:
 class SelfPlay:
     """self_play.py:21-219 with the games of one call played in lockstep on the GPU."""
 
-    def __init__(self, model, args: dict):
+    def __init__(self, model, args: dict, evaluator: Optional[Callable] = None):
+        """evaluator: the leaf evaluator (default: LeafEvaluator(model), the fp32 h2 kernel).
+        Any callable leaf_x -> (logits, value) works; with ``outputs_probs = True`` it returns
+        softmaxed rows instead of logits, and a ``bind(engine)`` method is called with each new
+        engine (tests replay the reference's recorded NN outputs this way)."""
         from .network import LeafEvaluator
         self.model = model
         self.device = next(model.parameters()).device
@@ -234,8 +248,9 @@ class SelfPlay:
             self.model = model.to(self.device)
         self.model.eval()
         self.args = args
-        self.evaluator = LeafEvaluator(self.model, dtype=args.get("nn_dtype", torch.float32),
-                                       device=self.device)
+        self.evaluator = evaluator if evaluator is not None else LeafEvaluator(
+            self.model, dtype=args.get("nn_dtype", torch.float32), device=self.device)
+        self.board_size = int(getattr(model, "board_size", 8))
         self.save_dir = args.get("save_dir", "self_play_data")
         os.makedirs(self.save_dir, exist_ok=True)
         self.seed = int(args.get("seed", 42))
@@ -244,24 +259,30 @@ class SelfPlay:
     def _play(self, num_games: int) -> List[Dict]:
         # compacted leaf batches: only the live leaves are evaluated (as _process_batch does);
         # the games are identical either way
+        bs = self.board_size
         eng = Engine(num_games, self.args.get("num_simulations", 800),
                      self.args.get("batch_size", 64), self.args.get("c_puct", 1.0),
-                     device=self.device,
+                     board_size=bs, device=self.device,
                      compact_leaves=bool(self.args.get("compact_leaves", True)))
+        if hasattr(self.evaluator, "bind"):
+            self.evaluator.bind(eng)
+        max_plies = bs * bs - 4         # every ply places a disc (passes are inside make_move)
         run = SelfPlayRunner(eng, self.evaluator, self.args.get("temperature", 1.0),
                              fused_softmax=self.args.get("fused_softmax", True),
-                             seed_base=self.seed + self.games_played, record=True)
+                             seed_base=self.seed + self.games_played, record=True,
+                             max_plies=max_plies)
         run.start()
-        for _ in range(60):             # every ply places a disc: <= 60 plies per game
+        for _ in range(max_plies):
             run.ply()
-        eng.check()
-        G = num_games
+        run.check()
+        if not bool(run.post_status[:, 1].all()):
+            raise RuntimeError(f"SelfPlay: a game is not over after {max_plies} plies")
+        G, P = num_games, max_plies
         black, white, side = run.rec_black, run.rec_white, run.rec_side
         st = torch.stack([side, torch.zeros_like(side), torch.full_like(side, -1),
                           torch.zeros_like(side)], dim=-1).reshape(-1, 4).contiguous()
         planes = board_canonical(black.reshape(-1).contiguous(), white.reshape(-1).contiguous(),
-                                 st, eng.board_size).reshape(60, G, 3, eng.board_size,
-                                                             eng.board_size)
+                                 st, bs).reshape(P, G, 3, bs, bs)
         planes, idx, p = planes.cpu().numpy(), run.rec_idx.cpu().numpy(), run.rec_p.cpu().numpy()
         side_h, final = side.cpu().numpy(), run.post_status.cpu().numpy()
         games = []
