@@ -18,6 +18,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "librvz_oracle.so")
+# RVZ_ORACLE_LIB: load another build of the same sources instead (tests/test_oracle_sanitize.py
+# points it at the ASan/UBSan build, librvz_oracle_san.so)
+_LIB_OVERRIDE = os.environ.get("RVZ_ORACLE_LIB")
 
 
 class Game(C.Structure):
@@ -52,7 +55,7 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        _lib = C.CDLL(build())
+        _lib = C.CDLL(_LIB_OVERRIDE or build())
         L = _lib
         u64, i32, f64 = C.c_uint64, C.c_int32, C.c_double
         L.rvzo_legal.restype = u64
