@@ -149,6 +149,7 @@ class LeafEvaluator:
     def __init__(self, net: AlphaZeroNetwork, dtype=torch.float32, device=None,
                  fused_epilogue: bool = None, kernel: str = "auto"):
         net = net.eval()
+        self.net = net
         dev = torch.device(device) if device is not None else next(net.parameters()).device
         self.dtype, self.device = dtype, dev
         # kernel: the whole forward in one rvz kernel (fp32, 8x8 or 6x6, 64/128 filters) —
@@ -231,6 +232,49 @@ class LeafEvaluator:
             for b in net.res_blocks:
                 trunk += [_fold(b.conv1, b.bn1)[1], _fold(b.conv2, b.bn2)[1]]
             self._b32 = [t.to(dev, torch.float32).contiguous() for t in trunk]
+
+    @torch.no_grad()
+    def refresh(self):
+        """Re-read the module's (trained) weights and BN statistics into this evaluator's device
+        buffers, in place: the addresses a captured HIP graph holds stay valid, so the next
+        replay evaluates the new net (the self-play / training loop, rvz.pipeline)."""
+        net = self.net
+        if self.use_resnet:
+            from . import _lib
+            self.params.copy_(pack_resnet_params(net).to(self.device))
+            if self.kernel == "h2":
+                _lib.check(_lib.load().rvz_resnet_h2_weights(
+                    self.params.data_ptr(), self.filters, self.n_blocks, self.wsplit.data_ptr(),
+                    _lib.stream_handle(self.device)), None, "rvz_resnet_h2_weights")
+            elif self.kernel == "split":
+                _lib.check(_lib.load().rvz_resnet_split_weights(
+                    self.params.data_ptr(), self.filters, self.n_blocks, self.wsplit.data_ptr(),
+                    _lib.stream_handle(self.device)), None, "rvz_resnet_split_weights")
+        cl, dt = torch.channels_last, self.dtype
+
+        def put(dst, conv, bn):
+            w, b = _fold(conv, bn)
+            dst[0].copy_(w.to(self.device, dt).contiguous(memory_format=cl))
+            dst[1].copy_(b.to(self.device, dt))
+
+        put(self.stem, net.conv, net.bn)
+        for (d1, d2), blk in zip(self.blocks, net.res_blocks):
+            put(d1, blk.conv1, blk.bn1)
+            put(d2, blk.conv2, blk.bn2)
+        put(self.pconv, net.policy_conv, net.policy_bn)
+        put(self.vconv, net.value_conv, net.value_bn)
+        cells = self.board_size ** 2
+        for dst, fc, planes in ((self.pfc, net.policy_fc, 2), (self.vfc1, net.value_fc1, 1)):
+            w = fc.weight.reshape(fc.out_features, planes, cells).permute(0, 2, 1)
+            dst[0].copy_(w.reshape(fc.out_features, planes * cells).to(self.device, dt))
+            dst[1].copy_(fc.bias.to(self.device, dt))
+        self.vfc2[0].copy_(net.value_fc2.weight.to(self.device, dt))
+        self.vfc2[1].copy_(net.value_fc2.bias.to(self.device, dt))
+        trunk = [_fold(net.conv, net.bn)[1]]
+        for b in net.res_blocks:
+            trunk += [_fold(b.conv1, b.bn1)[1], _fold(b.conv2, b.bn2)[1]]
+        for dst, t in zip(self._b32, trunk):
+            dst.copy_(t.to(self.device, torch.float32))
 
     def _bias_act(self, y: torch.Tensor, bias: torch.Tensor, res, relu: bool):
         from . import _lib

@@ -27,14 +27,18 @@ from .engine import board_canonical
 
 def records_to_training(rec_black: torch.Tensor, rec_white: torch.Tensor, rec_side: torch.Tensor,
                         rec_idx: torch.Tensor, rec_p: torch.Tensor, final_status: torch.Tensor,
-                        board_size: int = 8) -> Dict[str, torch.Tensor]:
+                        board_size: int = 8, canonical=None) -> Dict[str, torch.Tensor]:
     """Self-play records [plies, G] -> training arrays in the reference's layout and order.
 
     states f32 [n,3,S,S] (get_canonical_state of the position before each move), policy_targets
     f32 [n,S*S+1] (get_action_probs' p), value_targets f32 [n,1] = +1/-1/0 from the final winner
     relative to the player to move (self_play.py:117-126); games in order, plies in order
     (pipeline.py:179-246). Only plies that committed a move (rec_idx >= 0) are kept.
+    canonical(black, white, status, board_size) -> planes: default the rvz_board_canonical HIP
+    kernel (tests on a host without a GPU pass the oracle's restatement).
     """
+    if canonical is None:
+        canonical = board_canonical
     P, G = rec_idx.shape
     live = (rec_idx >= 0).t().reshape(-1)                    # game-major order
     black = rec_black.t().reshape(-1)[live].contiguous()
@@ -42,7 +46,7 @@ def records_to_training(rec_black: torch.Tensor, rec_white: torch.Tensor, rec_si
     side = rec_side.t().reshape(-1)[live]
     st = torch.stack([side, torch.zeros_like(side), torch.full_like(side, -1),
                       torch.zeros_like(side)], dim=1).to(torch.int32).contiguous()
-    states = board_canonical(black, white, st, board_size)
+    states = canonical(black, white, st, board_size)
     policy = rec_p.permute(1, 0, 2).reshape(P * G, -1)[live].to(torch.float32)
     winner = final_status[:, 2].to(torch.int32).unsqueeze(0).expand(P, G).t().reshape(-1)[live]
     over = final_status[:, 1].unsqueeze(0).expand(P, G).t().reshape(-1)[live]
@@ -71,6 +75,16 @@ class DDPTrainer:
         self.wp, self.wv = policy_loss_weight, value_loss_weight
         self.batch_size = batch_size
 
+    @torch.no_grad()
+    def sync_buffers(self):
+        """Broadcast rank 0's BN running statistics: DDP broadcasts buffers before each forward,
+        but the last forward of an epoch updates them locally, so without this the ranks would
+        self-play with slightly different nets."""
+        if not self.distributed:
+            return
+        for b in self.model.buffers():
+            dist.broadcast(b, 0)
+
     def rank_world(self):
         return (dist.get_rank(), dist.get_world_size()) if self.distributed else (0, 1)
 
@@ -90,17 +104,29 @@ class DDPTrainer:
         return loss.detach(), policy_loss.detach(), value_loss.detach()
 
     def train_epoch(self, data: Dict[str, torch.Tensor], seed: int = 0,
-                    max_steps: Optional[int] = None) -> Dict[str, float]:
-        """One pass over `data` (identical on every rank): each rank takes every world-th batch
-        of one seeded permutation. Returns the reference's averaged loss dict."""
+                    max_steps: Optional[int] = None, local_data: bool = False
+                    ) -> Dict[str, float]:
+        """One pass over the data. local_data=False: `data` is identical on every rank and each
+        rank takes every world-th batch of one seeded permutation. local_data=True: every rank
+        holds its own data (its own self-play games, rvz.pipeline) and walks its own permutation
+        (seed + rank). Either way each step's global batch is world x batch_size, and every rank
+        runs the same number of steps (the minimum over ranks). Returns the reference's averaged
+        loss dict (pipeline.py:342-366)."""
         rank, world = self.rank_world()
         n = data["states"].shape[0]
-        g = torch.Generator().manual_seed(seed)
+        g = torch.Generator().manual_seed(seed + (rank if local_data else 0))
         order = torch.randperm(n, generator=g)
+        if local_data:
+            rank, world = 0, 1        # indexing within this rank's own permutation
         per_step = self.batch_size * world
         steps = n // per_step
         if max_steps is not None:
             steps = min(steps, max_steps)
+        if self.distributed:          # every rank must run the same number of DDP steps
+            t = torch.tensor([steps], dtype=torch.int64,
+                             device=self.device if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            steps = int(t.item())
         tot = torch.zeros(3, dtype=torch.float64, device=self.device)
         for s in range(steps):
             idx = order[s * per_step + rank * self.batch_size:

@@ -40,7 +40,9 @@ PRESETS = {   # BASELINE.json configs (index 0 is the reference's own single CPU
     # lanes: independent game lanes per GPU in one graph (same games; measured best per config)
     "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2),
     "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),
-    "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),  # per GPU, x8
+    # per GPU, x8; a step = one self-play + training iteration (main_c4)
+    "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, steps=1,
+               warmup=0),
     "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2),
 }
 
@@ -50,10 +52,10 @@ def parse():
     ap.add_argument("--config", choices=sorted(PRESETS), default="c2",
                     help="BASELINE.json workload preset; explicit flags override it")
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60,
+    ap.add_argument("--steps", type=int, default=None,
                     help="timed plies; the default spans a whole 8x8 game (every stage, endgame "
                          "included): the steady-state mix of continuous self-play")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--games", type=int, default=None, help="games per GPU")
     ap.add_argument("--sims", type=int, default=None)
     ap.add_argument("--batch", type=int, default=64)
@@ -93,8 +95,12 @@ def parse():
                     help="nccl (= RCCL) for real multi-GPU runs; gloo to rehearse several ranks "
                          "on one device")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--train-steps", type=int, default=100,
+                    help="c4: DDP optimizer steps per iteration (batch --train-batch per rank)")
+    ap.add_argument("--train-batch", type=int, default=64,
+                    help="c4: per-rank training batch (TrainingConfig.batch_size = 64)")
     args = ap.parse_args()
-    for k, v in PRESETS[args.config].items():
+    for k, v in dict(dict(steps=60, warmup=3), **PRESETS[args.config]).items():
         if getattr(args, k) is None:
             setattr(args, k, v)
     return args
@@ -298,8 +304,146 @@ def cpu_baseline(args, net):
             "env_tree_only_1core": one}
 
 
+def main_c4(args):
+    """BASELINE.json config 4: self-play + training, one process per GPU (rvz.pipeline;
+    reference pipeline.py:114-150). A bench step is one ITERATION: every game of the rank from
+    the start position to its end (60 plies, captured ply graph), the device records turned into
+    training arrays, then --train-steps DDP steps whose gradient all-reduce runs over RCCL. value
+    = board-steps of all ranks / max-over-ranks wall time of the K iterations, training included.
+    The process group is created even at one rank (backend nccl = RCCL), so DDP's all-reduce runs
+    at every N."""
+    import socket
+
+    import torch.distributed as tdist
+
+    import rvz
+    from rvz import dist as rdist
+    from rvz.pipeline import SelfPlayTrainer
+
+    rank, local_rank, world = rdist.env_rank_world()
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    if not tdist.is_initialized():
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
+        tdist.init_process_group(backend=args.dist_backend, device_id=device
+                                 if args.dist_backend == "nccl" else None)
+    net = make_net(args, device)
+    n_params = sum(p.numel() for p in net.parameters())
+    spt = SelfPlayTrainer(net, args.games, args.sims, args.batch, 1.0, 1.0, seed=args.seed,
+                          train_steps=args.train_steps, train_batch=args.train_batch,
+                          graph=not args.no_graph, compact_leaves=not args.no_compact)
+    # warm-up (untimed): one eager ply, the ply graph captured, two DDP steps on stand-in data
+    run = spt.runner
+    run.start()
+    run.ply()
+    if not args.no_graph:
+        run.capture()
+    g = torch.Generator(device=device).manual_seed(rank)
+    warm = {"states": (torch.rand(4 * args.train_batch, 3, args.board, args.board, device=device,
+                                  generator=g) > 0.6).float(),
+            "policy_targets": torch.rand(4 * args.train_batch, args.board ** 2 + 1,
+                                         device=device, generator=g),
+            "value_targets": torch.zeros(4 * args.train_batch, 1, device=device)}
+    spt.trainer.train_epoch(warm, seed=0, max_steps=2, local_data=True)
+    spt.trainer.sync_buffers()
+    spt.evaluator.refresh()
+    for _ in range(args.warmup):
+        spt.run_iteration()
+    rdist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    its = [spt.run_iteration() for _ in range(args.steps)]
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    rdist.barrier()
+    steps = sum(r["board_steps"] for r in its)
+    total, dt, value = rdist.aggregate_rate(steps, t1 - t0)
+    sp_s = rdist.reduce_max(sum(r["selfplay_s"] for r in its))
+    tr_s = rdist.reduce_max(sum(r["train_s"] for r in its))
+    n_train = sum(r["steps"] for r in its)
+    sp_rate = rdist.reduce_sum(steps) / sp_s
+    # the gradient all-reduce alone: one flat fp32 bucket of every parameter (what DDP's single
+    # 25 MB bucket carries), HIP events on the current stream, 20 back-to-back collectives
+    buf = torch.randn(n_params, device=device)
+    tdist.all_reduce(buf)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    rdist.barrier()
+    a.record()
+    for _ in range(20):
+        tdist.all_reduce(buf)
+    b.record()
+    torch.cuda.synchronize(device)
+    ar_ms = rdist.reduce_max(a.elapsed_time(b) / 20)
+    # the dominant kernel (the trunk) in isolation: HIP events over 10 back-to-back launches
+    ev, eng = spt.evaluator, spt.eng
+    roof = None
+    if ev.kernel == "h2":
+        ev.trunk_only(eng.leaf_x)
+        a.record()
+        for _ in range(10):
+            ev.trunk_only(eng.leaf_x)
+        b.record()
+        torch.cuda.synchronize(device)
+        t_tr = a.elapsed_time(b) / 10
+        fl = ev.mfma_flops_per_row() * eng.n_games
+        ach = fl / (t_tr * 1e-3) / 1e12
+        roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma", "achieved": round(ach, 2),
+                "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
+                "frac": round(ach / MFMA_PEAK_TFLOPS["bf16"], 4), "traffic": None,
+                "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": eng.n_games,
+                "timing": "HIP events over 10 back-to-back full-batch launches after the timed "
+                          "region"}
+    spt.eng.check()
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, net)
+    if rank == 0:
+        out = {
+            "metric": f"self-play board-steps/sec @ {args.sims} sims/move, "
+                      f"{args.board}x{args.board} Reversi",
+            "value": round(value, 2), "unit": "board-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u64 rules + f32 NN (fp32 as 2-part f16 split on MFMA); fp32 training",
+            "data": "synthetic (start position, per-game seeds, random-init net trained in the "
+                    "loop)",
+            "config": {"workload": f"c4: self-play + training; {args.games} games/GPU x "
+                                   f"{args.sims} sims, {args.blocks}x{args.filters} ResNet, "
+                                   f"{args.board}x{args.board}; a step = one iteration "
+                                   f"(whole games, then {args.train_steps} DDP steps)",
+                       "games_per_gpu": args.games, "global_games": args.games * world,
+                       "sims": args.sims, "batch": args.batch,
+                       "nn": f"{args.blocks}x{args.filters}",
+                       "train_steps_per_iter": args.train_steps,
+                       "train_batch_per_rank": args.train_batch,
+                       "parallelism": f"games sharded x{world}; DDP x{world} "
+                                      f"({tdist.get_backend()})"},
+            "selfplay_board_steps_per_s": round(sp_rate, 2),
+            "selfplay_s": round(sp_s, 3), "train_s": round(tr_s, 3),
+            "ms_per_train_step": round(tr_s / max(1, n_train) * 1e3, 3),
+            "allreduce": {"backend": tdist.get_backend(), "world": world,
+                          "bytes": n_params * 4, "ms": round(ar_ms, 4),
+                          "algbw_GBs": round(n_params * 4 / (ar_ms * 1e-3) / 1e9, 1)},
+            "train_loss": [round(r["train/loss"], 4) for r in its],
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    tdist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.config == "c4":
+        return main_c4(args)
     import rvz
     from rvz import dist as rdist
 
