@@ -1,1141 +1,17 @@
-// rvz_resnet.hip — the whole policy/value ResNet forward of the reference (network.py:30-117) in
-// ONE gfx950 kernel per leaf batch, in two fp32-class numerics:
-//
-//  * k_resnet_fwd (rvz_resnet_fwd_f32): the f32-input MFMA v_mfma_f32_32x32x2_f32 — bit-for-bit
-//    k-ordered fp32 FMA chains, the reference's precision, at the f32 matrix rate (157 TF/s).
-//  * k_resnet_split (rvz_resnet_fwd_split): every fp32 operand split exactly into three bf16
-//    parts, x = x0 + (x1 + x2) (8 significant bits each, 24 together), and the conv GEMMs run on
-//    v_mfma_f32_16x16x32_bf16 (16x the f32 rate) with the six partial products whose weight is
-//    >= 2^-16: x0w0 into one fp32 accumulator, x0w1 + x1w0 + x1w1 + x0w2 + x2w0 into a second.
-//    The dropped terms (x1w2, x2w1, x2w2) are <= ~2^-24 of |x w|, i.e. below one fp32 rounding of
-//    the product, so the error matches an fp32 GEMM's (tests/test_gpu_network.py measures both
-//    against fp64). This is fp32 arithmetic emulated on the bf16 matrix cores, not a bf16 net:
-//    activations stay fp32 between layers (stored as their exact 3-part split), weights are
-//    split once per parameter update (rvz_resnet_split_weights).
+// rvz_resnet.hip — the reference's policy/value ResNet forward (network.py:30-117, BN folded) as
+// the rvz leaf evaluator on gfx950: ONE trunk kernel per leaf batch (k_resnet_h2: stem, residual
+// tower and 1x1 head convs, activations resident in LDS) plus one batched FC-heads launch
+// (k_heads_mfma, rvz_resnet_common.hip.h), fp32-class arithmetic on the f16 matrix cores.
 //
 // Why one kernel: with MIOpen, every conv layer is a separate launch plus a zero-fill of its
 // output and a bias/skip/ReLU pass, and every activation makes an HBM round trip. Here a
 // workgroup keeps its boards' activations in LDS for the whole network: HBM traffic is the leaf
-// planes in and the logits/value out; weights stream from L2 (shared by every workgroup).
-//
-// f32 kernel layout (one workgroup = 4 waves = NBOARD boards; F filters; 8x8 boards):
-//   LDS act[2][NBOARD][64 pixels][F + 4 floats]   (ping-pong h / y; no halo: taps that leave the
-//   board are masked to 0). A pixel row is F + 4 floats, so consecutive pixels start 4 banks apart.
-//   conv layer = GEMM  M = NBOARD*64 pixels, N = F, K = 9 taps x F channels, on
-//   v_mfma_f32_32x32x2_f32: A lane l = (pixel l&31 of a 32-pixel M-tile, k-slot l>>5), B lane l =
-//   (k-slot l>>5, channel l&31 of the N-tile); k-slot h of step s is input channel h*(F/2)+s, so
-//   one ds_read_b128 (A) / global_load_dwordx4 (B) feeds 4 steps. Every 16-lane group of a
-//   ds_read_b128 then reads 16 distinct consecutive pixels: bank-conflict free (a 16x16x4 layout
-//   mixed k-slots inside a group: 61% of its LDS cycles were conflicts, rocprof SQ_LDS_BANK_CONFLICT).
-//   Wave w: N-tile, 2 M-tiles -> 2 accumulators of 16 floats.
-// Split kernel layout: see CfgS / conv_split below.
-// Packed parameter buffer (fp32, BN folded by rvz.LeafEvaluator; every segment starts 16-byte
-// aligned; offsets in make_layout):
-//   stem_w[F][27] (k = tap*3 + ch), stem_b[F], res_w[2NB][9][F(n)][F(k)], res_b[2NB][F],
-//   pol_w[2][F], pol_b[2], pfc_w[65][128] (in = c*64 + px), pfc_b[65], val_w[F], val_b[1],
-//   vfc1_w[256][64], vfc1_b[256], vfc2_w[256], vfc2_b[1].
-#include <hip/hip_runtime.h>
-#include <math.h>
-#include <stdint.h>
-
-#include "../../include/rvz.h"
-
+// planes in and the head-conv outputs out; weights stream from L2 (shared by every workgroup).
+// The A/B alternatives (exact f32 MFMA, 3-part bf16 split, VALU heads, the MIOpen epilogue) are
+// built into tools/alt/librvz_alt.so, not into this library.
+#include "rvz_resnet_common.hip.h"
 
 namespace {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-struct Layout {
-    int64_t stem_w, stem_b, res_w, res_b, pol_w, pol_b, pfc_w, pfc_b, val_w, val_b, vfc1_w,
-        vfc1_b, vfc2_w, vfc2_b, total;
-};
-
-__host__ __device__ inline int64_t al4(int64_t o) { return (o + 3) & ~int64_t(3); }
-
-__host__ __device__ inline Layout make_layout(int F, int NB, int BS = 8) {
-    Layout L;
-    const int cells = BS * BS;
-    int64_t o = 0;
-    L.stem_w = o; o = al4(o + (int64_t)F * 27);
-    L.stem_b = o; o = al4(o + F);
-    L.res_w = o;  o = al4(o + (int64_t)2 * NB * 9 * F * F);
-    L.res_b = o;  o = al4(o + (int64_t)2 * NB * F);
-    L.pol_w = o;  o = al4(o + 2 * F);
-    L.pol_b = o;  o = al4(o + 2);
-    L.pfc_w = o;  o = al4(o + (int64_t)(cells + 1) * 2 * cells);
-    L.pfc_b = o;  o = al4(o + cells + 1);
-    L.val_w = o;  o = al4(o + F);
-    L.val_b = o;  o = al4(o + 1);
-    L.vfc1_w = o; o = al4(o + 256 * cells);
-    L.vfc1_b = o; o = al4(o + 256);
-    L.vfc2_w = o; o = al4(o + 256);
-    L.vfc2_b = o; o = al4(o + 1);
-    L.total = o;
-    return L;
-}
-
-// ---------------------------------------------------------------------------------------------
-// exact 3-part bf16 split of an fp32 value
-
-__device__ __forceinline__ uint32_t bf16_rne(float x) {      // finite x
-    const uint32_t u = __float_as_uint(x);
-    return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
-__device__ __forceinline__ float bf16_f(uint32_t h) { return __uint_as_float(h << 16); }
-
-// x == h0 + (h1 + h2) exactly: x - h0 is exact (Sterbenz), carries <= 16 significant bits, and
-// its remainder after rounding to 8 bits carries <= 8, so h2 is exact too.
-__device__ __forceinline__ void split3(float x, uint16_t& h0, uint16_t& h1, uint16_t& h2) {
-    const uint32_t b0 = bf16_rne(x);
-    const float r1 = x - bf16_f(b0);
-    const uint32_t b1 = bf16_rne(r1);
-    const float r2 = r1 - bf16_f(b1);
-    h0 = (uint16_t)b0;
-    h1 = (uint16_t)b1;
-    h2 = (uint16_t)bf16_rne(r2);
-}
-__device__ __forceinline__ float join3(uint16_t h0, uint16_t h1, uint16_t h2) {
-    return bf16_f(h0) + (bf16_f(h1) + bf16_f(h2));
-}
-
-// the same split for two values with v_cvt_pk_bf16_f32 (round to nearest even, as bf16_rne)
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 bf16x2_f(uint32_t h) {
-    return f32x2{__uint_as_float(h << 16), __uint_as_float(h & 0xFFFF0000u)};
-}
-__device__ __forceinline__ uint32_t cvt2(f32x2 x) {
-    const bf16x2 b = __builtin_convertvector(x, bf16x2);
-    return __builtin_bit_cast(uint32_t, b);
-}
-__device__ __forceinline__ void split3x2(f32x2 x, uint32_t& h0, uint32_t& h1, uint32_t& h2) {
-    h0 = cvt2(x);
-    const f32x2 r1 = x - bf16x2_f(h0);
-    h1 = cvt2(r1);
-    h2 = cvt2(r1 - bf16x2_f(h1));
-}
-
-// ---------------------------------------------------------------------------------------------
-// activation accessors: the stem writes, the heads read, through these
-
-struct ActF32 {
-    float* p;
-    int cs;
-    __device__ void store(int row, int n, float v) const { p[row * cs + n] = v; }
-    __device__ float load(int row, int k) const { return p[row * cs + k]; }
-    __device__ void load8(int row, int k0, float (&v)[8]) const {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(p + row * cs + k0);
-        const f32x4 b = *reinterpret_cast<const f32x4*>(p + row * cs + k0 + 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
-    }
-};
-
-struct ActSplit {
-    uint16_t* p;
-    int cs, plane;
-    __device__ void store(int row, int n, float v) const {
-        uint16_t a, b, c;
-        split3(v, a, b, c);
-        uint16_t* o = p + row * cs + n;
-        o[0] = a;
-        o[plane] = b;
-        o[2 * plane] = c;
-    }
-    __device__ float load(int row, int k) const {
-        const uint16_t* o = p + row * cs + k;
-        return join3(o[0], o[plane], o[2 * plane]);
-    }
-    __device__ void load8(int row, int k0, float (&v)[8]) const {
-        typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
-        const uint16_t* o = p + row * cs + k0;
-        const u16x8 a = *reinterpret_cast<const u16x8*>(o);
-        const u16x8 b = *reinterpret_cast<const u16x8*>(o + plane);
-        const u16x8 c = *reinterpret_cast<const u16x8*>(o + 2 * plane);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = join3(a[j], b[j], c[j]);
-    }
-};
-
-// leaf planes x[g][3][BS][BS] -> xin[b][10x10 padded pixel][4] (halo and, for BS < 8, the
-// unused rows/columns 0)
-template <int NBOARD, int BS = 8>
-__device__ __forceinline__ void load_input(const float* __restrict__ x, int n_boards, int g0,
-                                           float* xin, int tid, int nthr) {
-    constexpr int CELLS = BS * BS;
-    for (int i = tid; i < NBOARD * 100 * 4; i += nthr) xin[i] = 0.0f;
-    __syncthreads();
-    for (int i = tid; i < NBOARD * 3 * CELLS; i += nthr) {
-        const int b = i / (3 * CELLS), rem = i % (3 * CELLS), ch = rem / CELLS,
-                  cell = rem % CELLS;
-        const int g = g0 + b;
-        const float v = g < n_boards ? x[(size_t)g * 3 * CELLS + rem] : 0.0f;
-        xin[(b * 100 + (cell / BS + 1) * 10 + (cell % BS) + 1) * 4 + ch] = v;
-    }
-}
-
-// stem: conv 3 -> F (VALU; 0.4% of the FLOPs), bias, ReLU -> act rows b*64 + px.
-// Lane = pixel (the 27 input taps read from LDS once), wave = (board, group of channels) with the
-// group's weights wave-uniform (scalar loads).
-template <int F, int NBOARD, int NTHR, class Act>
-__device__ __forceinline__ void stem(const float* xin, const Act& act, const float* __restrict__ prm,
-                                     const Layout& L, int tid) {
-    constexpr int NW = NTHR / 64, CG = NW / NBOARD, CPG = F / CG;
-    static_assert(NW % NBOARD == 0 && F % CG == 0, "wave -> (board, channel group)");
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), px = tid & 63;
-    const int b = wave % NBOARD, cg = wave / NBOARD, r = px >> 3, c = px & 7;
-    float in[27];
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch)
-            in[t * 3 + ch] = xin[(b * 100 + (r + t / 3) * 10 + (c + t % 3)) * 4 + ch];
-    const float* w = prm + L.stem_w + (int64_t)cg * CPG * 27;
-    const float* bias = prm + L.stem_b + cg * CPG;
-#pragma unroll 4
-    for (int j = 0; j < CPG; ++j) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 27; ++k) acc = fmaf(in[k], w[j * 27 + k], acc);
-        act.store(b * 64 + px, cg * CPG + j, fmaxf(acc + bias[j], 0.0f));
-    }
-}
-
-// heads (network.py:104-117), part 1: the 1x1 convs (BN folded) + ReLU of both heads, in one
-// pass over the activations: lane = pixel, wave = (board, channel group), partial sums per group
-// through LDS (`part`, the free ping-pong buffer) added in a fixed order. Writes, per board b
-// (cells = BS*BS), hpv(b)[0 .. 2 cells) = the policy planes (NCHW flatten, the FC's input order)
-// and hpv(b)[2 cells .. 3 cells) = the value plane. A BS < 8 board sits in the top-left corner
-// of the 8x8 pixel grid.
-template <int F, int NBOARD, int NTHR, int BS = 8, bool PACKED = false, class Act, class Out>
-__device__ __forceinline__ void head_convs(const Act& act, float* part,
-                                           const float* __restrict__ prm, const Layout& L,
-                                           const Out& hpv, int tid) {
-    constexpr int NW = NTHR / 64, CG = NW / NBOARD, CPG = F / CG;
-    static_assert(CPG % 8 == 0, "8-channel reads");
-    const int lane = tid & 63;
-    {
-        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-        // PACKED: board b's cells are act rows b * BS^2 + cell (h2); else the 8x8 grid
-        const int b = wave % NBOARD, cg = wave / NBOARD, row = b * 64 + lane;
-        const int arow = PACKED ? b * BS * BS + lane : row;
-        const bool on = !PACKED || lane < BS * BS;
-        const float* w0 = prm + L.pol_w + cg * CPG;
-        const float* w1 = w0 + F;
-        const float* w2 = prm + L.val_w + cg * CPG;
-        float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
-#pragma unroll
-        for (int k8 = 0; k8 < CPG / 8; ++k8) {
-            if (!on) break;
-            float v[8];
-            act.load8(arow, cg * CPG + 8 * k8, v);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                p0 = fmaf(v[j], w0[8 * k8 + j], p0);
-                p1 = fmaf(v[j], w1[8 * k8 + j], p1);
-                p2 = fmaf(v[j], w2[8 * k8 + j], p2);
-            }
-        }
-        part[(cg * 3 + 0) * NBOARD * 64 + row] = p0;
-        part[(cg * 3 + 1) * NBOARD * 64 + row] = p1;
-        part[(cg * 3 + 2) * NBOARD * 64 + row] = p2;
-    }
-    __syncthreads();
-    constexpr int CELLS = BS * BS;
-    for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
-        const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
-        const int b = rem / CELLS, cell = rem % CELLS;
-        const int row = b * 64 + (PACKED ? cell : (cell / BS) * 8 + cell % BS);
-        float acc = 0.0f;
-#pragma unroll
-        for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * NBOARD * 64 + row];
-        const float bias = c2 < 2 ? prm[L.pol_b + c2] : prm[L.val_b];
-        hpv.store(b, c2 * CELLS + cell, fmaxf(acc + bias, 0.0f));
-    }
-}
-
-struct HeadsLds {        // hpv rows in LDS
-    float* p;
-    __device__ void store(int b, int i, float v) const { p[b * 192 + i] = v; }
-};
-struct HeadsGlobal {     // hpv rows in the global workspace of rvz_resnet_fwd_split
-    float* p;
-    int g0, n_boards;
-    __device__ void store(int b, int i, float v) const {
-        if (g0 + b < n_boards) p[(size_t)(g0 + b) * 192 + i] = v;
-    }
-};
-
-// heads, part 2 (in-kernel form): policy fc (2 cells -> cells + 1), value fc1 (cells -> 256,
-// ReLU), value fc2 (256 -> 1) + tanh, for the NBOARD boards of a workgroup; hpv in LDS (rows of
-// 192: policy planes, then the value plane)
-template <int NBOARD, int NTHR, int BS = 8>
-__device__ __forceinline__ void head_fcs(const float* hpv, float* h1,
-                                         const float* __restrict__ prm, const Layout& L, int g0,
-                                         int n_boards, float* __restrict__ logits,
-                                         float* __restrict__ value, int tid) {
-    constexpr int CELLS = BS * BS, POUT = CELLS + 1, PIN = 2 * CELLS, ROWS = POUT + 256;
-    const int lane = tid & 63;
-    // thread per output row, f32x4 loads
-    for (int o = tid; o < NBOARD * ROWS; o += NTHR) {
-        const int b = o / ROWS, rem = o % ROWS;
-        const int g = g0 + b;
-        if (rem < POUT) {
-            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.pfc_w + rem * PIN);
-            const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192);
-            float acc = prm[L.pfc_b + rem];
-#pragma unroll 16
-            for (int i = 0; i < PIN / 4; ++i) {
-                const f32x4 w = wr[i], v = in[i];
-                acc = fmaf(v[0], w[0], acc);
-                acc = fmaf(v[1], w[1], acc);
-                acc = fmaf(v[2], w[2], acc);
-                acc = fmaf(v[3], w[3], acc);
-            }
-            if (g < n_boards) logits[(size_t)g * POUT + rem] = acc;
-        } else {
-            const int u = rem - POUT;
-            const f32x4* wr = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + u * CELLS);
-            const f32x4* in = reinterpret_cast<const f32x4*>(hpv + b * 192 + PIN);
-            float acc = prm[L.vfc1_b + u];
-#pragma unroll
-            for (int i = 0; i < CELLS / 4; ++i) {
-                const f32x4 w = wr[i], v = in[i];
-                acc = fmaf(v[0], w[0], acc);
-                acc = fmaf(v[1], w[1], acc);
-                acc = fmaf(v[2], w[2], acc);
-                acc = fmaf(v[3], w[3], acc);
-            }
-            h1[b * 256 + u] = fmaxf(acc, 0.0f);
-        }
-    }
-    __syncthreads();
-    // value fc2 (256 -> 1) + tanh: one wave per board
-    const int wave = tid >> 6;
-    for (int b = wave; b < NBOARD; b += NTHR / 64) {
-        float acc = 0.0f;
-        for (int i = lane; i < 256; i += 64) acc = fmaf(h1[b * 256 + i], prm[L.vfc2_w + i], acc);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-        const int g = g0 + b;
-        if (lane == 0 && g < n_boards) value[g] = tanhf(acc + prm[L.vfc2_b]);
-    }
-}
-
-// heads, part 2 as its own launch over FCB boards per workgroup (the split path): each FC weight
-// row is loaded once per workgroup into registers and applied to all FCB boards (LDS broadcast
-// inputs) — inside the trunk kernel the same weights streamed from L2 once per 2 boards, with
-// the matrix cores idle. Thread t: value-fc1 row t; threads < 2*(cells+1): half of policy row
-// t/2. work rows: [2 cells policy planes | cells value plane], stride 192.
-#ifndef RVZ_FCB
-#define RVZ_FCB 8
-#endif
-constexpr int FCB = RVZ_FCB;   // boards per workgroup (multiple of 4)
-static_assert(RVZ_LIVE_STRIPE % FCB == 0 && RVZ_LIVE_STRIPE % 16 == 0, "stripe granules");
-
-// a compacted leaf batch (include/rvz.h RVZ_LIVE_STRIPE): is the row past its stripe's live count?
-__device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int row) {
-    return n_live && row % RVZ_LIVE_STRIPE >= n_live[row / RVZ_LIVE_STRIPE * RVZ_LIVE_PITCH];
-}
-template <int BS>
-__global__ __launch_bounds__(256) void k_heads_fc(const float* __restrict__ work, int n,
-                                                  const float* __restrict__ prm, Layout L,
-                                                  float* __restrict__ logits,
-                                                  float* __restrict__ value,
-                                                  const int32_t* __restrict__ n_live,
-                                                  uint32_t* __restrict__ stamp_ctr) {
-    // bench.py: the trunk launch before this one is complete; advance its stamp ring
-    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
-    if (row_dead(n_live, (int)blockIdx.x * FCB)) return;   // the workgroup's rows are all dead
-    constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1, ROW = 3 * CELLS;
-    constexpr int VQ = CELLS / 4, PQ = PIN / 2 / 4;   // f32x4 per value row / policy half-row
-    static_assert(CELLS % 4 == 0 && 2 * POUT <= 256, "thread map");
-    __shared__ __attribute__((aligned(16))) float in[FCB][ROW];
-    __shared__ __attribute__((aligned(16))) float h1[FCB][256];
-    __shared__ float pp[FCB][2 * POUT];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g0 = blockIdx.x * FCB, nb = n - g0 < FCB ? n - g0 : FCB;
-    f32x4 wv[VQ], wp[PQ];
-    {
-        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.vfc1_w + tid * CELLS);
-#pragma unroll
-        for (int i = 0; i < VQ; ++i) wv[i] = r[i];
-    }
-    if (tid < 2 * POUT) {
-        const f32x4* r = reinterpret_cast<const f32x4*>(prm + L.pfc_w + (tid >> 1) * PIN +
-                                                         (tid & 1) * (PIN / 2));
-#pragma unroll
-        for (int i = 0; i < PQ; ++i) wp[i] = r[i];
-    }
-    for (int i = tid; i < FCB * ROW; i += 256) {
-        const int b = i / ROW, k = i % ROW;
-        (&in[0][0])[i] = b < nb ? work[(size_t)(g0 + b) * 192 + k] : 0.0f;
-    }
-    __syncthreads();
-    // 4 boards at a time: four independent FMA chains per thread
-    constexpr int IL = 4;
-    const float b1 = prm[L.vfc1_b + tid];
-    for (int b0 = 0; b0 < FCB; b0 += IL) {
-        float acc[IL];
-#pragma unroll
-        for (int j = 0; j < IL; ++j) acc[j] = b1;
-#pragma unroll
-        for (int i = 0; i < VQ; ++i)
-#pragma unroll
-            for (int j = 0; j < IL; ++j) {
-                const f32x4 x = reinterpret_cast<const f32x4*>(&in[b0 + j][PIN])[i];
-                acc[j] = fmaf(x[0], wv[i][0], acc[j]);
-                acc[j] = fmaf(x[1], wv[i][1], acc[j]);
-                acc[j] = fmaf(x[2], wv[i][2], acc[j]);
-                acc[j] = fmaf(x[3], wv[i][3], acc[j]);
-            }
-#pragma unroll
-        for (int j = 0; j < IL; ++j) h1[b0 + j][tid] = fmaxf(acc[j], 0.0f);
-    }
-    if (tid < 2 * POUT) {
-        for (int b0 = 0; b0 < FCB; b0 += IL) {
-            float acc[IL] = {};
-#pragma unroll
-            for (int i = 0; i < PQ; ++i)
-#pragma unroll
-                for (int j = 0; j < IL; ++j) {
-                    const f32x4 x =
-                        reinterpret_cast<const f32x4*>(&in[b0 + j][(tid & 1) * (PIN / 2)])[i];
-                    acc[j] = fmaf(x[0], wp[i][0], acc[j]);
-                    acc[j] = fmaf(x[1], wp[i][1], acc[j]);
-                    acc[j] = fmaf(x[2], wp[i][2], acc[j]);
-                    acc[j] = fmaf(x[3], wp[i][3], acc[j]);
-                }
-#pragma unroll
-            for (int j = 0; j < IL; ++j) pp[b0 + j][tid] = acc[j];
-        }
-    }
-    __syncthreads();
-    for (int o = tid; o < nb * POUT; o += 256) {
-        const int b = o / POUT, r = o % POUT;
-        logits[(size_t)(g0 + b) * POUT + r] =
-            prm[L.pfc_b + r] + (pp[b][2 * r] + pp[b][2 * r + 1]);
-    }
-    for (int b = wave; b < nb; b += 4) {
-        float acc = 0.0f;
-        for (int i = lane; i < 256; i += 64) acc = fmaf(h1[b][i], prm[L.vfc2_w + i], acc);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-        if (lane == 0) value[g0 + b] = tanhf(acc + prm[L.vfc2_b]);
-    }
-}
-
-// heads, part 2 on the f32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
-// accumulation — the arithmetic of an fp32 GEMM), 16 boards per workgroup: D = W X^T with rows =
-// output units (16-unit tiles: value fc1 16 tiles, policy fc ceil((cells+1)/16)), columns = the
-// 16 boards. The K order is permuted (step 4j + i uses k = 16j + 4g + i for lane group
-// g = lane >> 4), so a lane loads 4 consecutive k of its weight row (f32x4, L2) and of its
-// board's input row (ds_read_b128) per 4 MFMAs. Value fc2 (256 -> 1) + tanh reduce the fc1 tiles
-// through registers, lane shuffles and 64 floats of LDS.
-template <int BS>
-__global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ work, int n,
-                                                    const float* __restrict__ prm, Layout L,
-                                                    float* __restrict__ logits,
-                                                    float* __restrict__ value,
-                                                    const int32_t* __restrict__ n_live,
-                                                    uint32_t* __restrict__ stamp_ctr) {
-    // bench.py: the trunk launch before this one is complete; advance its stamp ring
-    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
-    if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
-    constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
-    constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
-    constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
-    constexpr int VJ = VK / 16, PJ = PK / 16, VTW = 256 / 16 / 4, PTW = (PT + 3) / 4;
-    static_assert(CELLS % 4 == 0 && PIN % 4 == 0, "f32x4 rows");
-    __shared__ __attribute__((aligned(16))) float in[16 * ROW];
-    __shared__ float vpart[4][16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g0 = blockIdx.x * 16, col = lane & 15, grp = lane >> 4;
-    // every weight fragment of this wave's tiles, issued before anything waits: value fc1 tiles
-    // wave + 4m, policy tiles wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
-    f32x4 av[VTW][VJ], ap[PTW][PJ];
-#pragma unroll
-    for (int m = 0; m < VTW; ++m) {
-        const float* wr = prm + L.vfc1_w + (size_t)(16 * (wave + 4 * m) + col) * CELLS + 4 * grp;
-#pragma unroll
-        for (int j = 0; j < VJ; ++j)
-            av[m][j] = 16 * j + 4 * grp < CELLS ? *reinterpret_cast<const f32x4*>(wr + 16 * j)
-                                                : f32x4{};
-    }
-#pragma unroll
-    for (int m = 0; m < PTW; ++m) {
-        const int o = 16 * (wave + 4 * m) + col;
-        const float* wr = prm + L.pfc_w + (size_t)o * PIN + 4 * grp;
-#pragma unroll
-        for (int j = 0; j < PJ; ++j)
-            ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
-                           ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
-    }
-    for (int i = tid; i < 16 * (PK + VK); i += 256) {
-        const int b = i / (PK + VK), k = i % (PK + VK), g = g0 + b;
-        float v = 0.0f;
-        if (g < n) {
-            if (k < PIN) v = work[(size_t)g * 192 + k];
-            else if (k >= PK && k - PK < CELLS) v = work[(size_t)g * 192 + PIN + (k - PK)];
-        }
-        in[b * ROW + k] = v;
-    }
-    __syncthreads();
-    const float* inb = in + col * ROW + 4 * grp;
-    // value fc1 (+ bias, ReLU) and its fc2 partial
-    float vp = 0.0f;
-#pragma unroll
-    for (int m = 0; m < VTW; ++m) {
-        f32x4 acc = {};
-#pragma unroll
-        for (int j = 0; j < VJ; ++j) {
-            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + PK + 16 * j);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][j][i], bx[i], acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {                // D row = unit 16t + 4grp + r, col = board
-            const int uu = 16 * (wave + 4 * m) + 4 * grp + r;
-            vp = fmaf(fmaxf(acc[r] + prm[L.vfc1_b + uu], 0.0f), prm[L.vfc2_w + uu], vp);
-        }
-    }
-    vp += __shfl_xor(vp, 16);
-    vp += __shfl_xor(vp, 32);
-    if (grp == 0) vpart[wave][col] = vp;
-    // policy fc
-#pragma unroll
-    for (int m = 0; m < PTW; ++m) {
-        const int t = wave + 4 * m;
-        if (t >= PT) break;
-        f32x4 acc = {};
-#pragma unroll
-        for (int j = 0; j < PJ; ++j) {
-            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + 16 * j);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[m][j][i], bx[i], acc, 0, 0, 0);
-        }
-        const int g = g0 + col;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int oo = 16 * t + 4 * grp + r;
-            if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
-        }
-    }
-    __syncthreads();
-    if (tid < 16 && g0 + tid < n)
-        value[g0 + tid] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
-                                prm[L.vfc2_b]);
-}
-
-// =============================================================================================
-// f32 MFMA kernel
-
-template <int F, int NBOARD>
-struct Cfg {
-    static constexpr int CS = F + 4;                 // padded channel stride (bank spread)
-    static constexpr int BOARD = 64 * CS;            // floats per board per buffer
-    static constexpr int ACT = NBOARD * BOARD;       // floats per buffer
-    static constexpr int XIN = NBOARD * 100 * 4;     // stem input, 3 planes padded to 4 (halo)
-    static constexpr int HPV = NBOARD * 192;         // 1x1 conv outputs (policy NCHW, value)
-    static constexpr int H1 = NBOARD * 256;          // value fc1 output
-    static constexpr int SMEM = 2 * ACT + XIN + HPV + H1;
-    static constexpr int MTILES = 2 * NBOARD;        // 32-pixel M-tiles (4 board rows each)
-    static constexpr int NTILES = F / 32;            // 32-channel N-tiles
-    static_assert(MTILES * NTILES == 8, "8 tiles = 4 waves x 2 accumulators");
-    static_assert(SMEM * 4 <= 160 * 1024, "fits the 160 KiB LDS of a CU");
-};
-
-// One 3x3 conv layer: out = relu(conv(in) + bias (+ res)), all in LDS.
-template <int F, int NBOARD, bool RES>
-__device__ __forceinline__ void conv_layer(const float* __restrict__ in, float* __restrict__ out,
-                                           const float* __restrict__ w,   // [9][F][F]
-                                           const float* __restrict__ bias, int wave, int lane) {
-    using C = Cfg<F, NBOARD>;
-    constexpr int KH = F / 2;                     // steps per tap (2 k-slots)
-    // wave -> (N-tile, first M-tile): F=64: 2 N-tiles x 4 M-tiles; F=128: 4 N-tiles x 2 M-tiles
-    const int nt = F == 64 ? (wave & 1) : wave;
-    const int mt0 = F == 64 ? 2 * (wave >> 1) : 0;
-    const int h = lane >> 5, m = lane & 31;
-    f32x16 acc0 = {}, acc1 = {};
-    // A: pixel (mt*32 + m) of the workgroup; B: channel nt*32 + m
-    const int pix0 = mt0 * 32 + m, pix1 = pix0 + 32;
-    const int r0 = (pix0 & 63) >> 3, c0 = pix0 & 7, r1 = (pix1 & 63) >> 3, c1 = pix1 & 7;
-    const float* brow = w + (size_t)(nt * 32 + m) * F + h * KH;
-    const int koff = h * KH;
-    for (int t = 0; t < 9; ++t) {
-        const int dr = t / 3 - 1, dc = t % 3 - 1;
-        const bool v0 = (unsigned)(r0 + dr) < 8u && (unsigned)(c0 + dc) < 8u;
-        const bool v1 = (unsigned)(r1 + dr) < 8u && (unsigned)(c1 + dc) < 8u;
-        // out-of-board taps read their own pixel and are zeroed (no halo in LDS)
-        const float* a0p = in + (size_t)(v0 ? pix0 + dr * 8 + dc : pix0) * C::CS + koff;
-        const float* a1p = in + (size_t)(v1 ? pix1 + dr * 8 + dc : pix1) * C::CS + koff;
-        const float* bp = brow + (size_t)t * F * F;
-#pragma unroll 4
-        for (int g = 0; g < KH; g += 4) {
-            const f32x4 bv = *reinterpret_cast<const f32x4*>(bp + g);
-            f32x4 a0 = *reinterpret_cast<const f32x4*>(a0p + g);
-            f32x4 a1 = *reinterpret_cast<const f32x4*>(a1p + g);
-            if (!v0) a0 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            if (!v1) a1 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], bv[s], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], bv[s], acc1, 0, 0, 0);
-            }
-        }
-    }
-    // epilogue: D col = lane&31 (channel), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (pixel)
-    const int n = nt * 32 + m;
-    const float bn = bias[n];
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const int o0 = (mt0 * 32 + row) * C::CS + n, o1 = o0 + 32 * C::CS;
-        float x0 = acc0[reg] + bn, x1 = acc1[reg] + bn;
-        if (RES) { x0 += out[o0]; x1 += out[o1]; }   // skip input h, read then overwritten in place
-        out[o0] = fmaxf(x0, 0.0f);
-        out[o1] = fmaxf(x1, 0.0f);
-    }
-}
-
-template <int F, int NBOARD>
-__global__ __launch_bounds__(256, 2) void k_resnet_fwd(const float* __restrict__ x, int n_boards,
-                                                       const float* __restrict__ prm, Layout L,
-                                                       int n_blocks, float* __restrict__ logits,
-                                                       float* __restrict__ value) {
-    using C = Cfg<F, NBOARD>;
-    __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
-    float* actA = smem;
-    float* actB = smem + C::ACT;
-    float* xin = smem + 2 * C::ACT;
-    float* hpv = xin + C::XIN;
-    float* h1 = hpv + C::HPV;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g0 = blockIdx.x * NBOARD;
-
-    load_input<NBOARD>(x, n_boards, g0, xin, tid, 256);
-    __syncthreads();
-    stem<F, NBOARD, 256>(xin, ActF32{actA, C::CS}, prm, L, tid);
-    __syncthreads();
-    for (int blk = 0; blk < n_blocks; ++blk) {
-        const int l1 = 2 * blk, l2 = 2 * blk + 1;
-        conv_layer<F, NBOARD, false>(actA, actB, prm + L.res_w + (size_t)l1 * 9 * F * F,
-                                     prm + L.res_b + (size_t)l1 * F, wave, lane);
-        __syncthreads();
-        conv_layer<F, NBOARD, true>(actB, actA, prm + L.res_w + (size_t)l2 * 9 * F * F,
-                                    prm + L.res_b + (size_t)l2 * F, wave, lane);
-        __syncthreads();
-    }
-    head_convs<F, NBOARD, 256>(ActF32{actA, C::CS}, actB, prm, L, HeadsLds{hpv}, tid);
-    __syncthreads();
-    head_fcs<NBOARD, 256>(hpv, h1, prm, L, g0, n_boards, logits, value, tid);
-}
-
-// =============================================================================================
-// split (3 x bf16) kernel
-//
-// LDS: act[2 buffers][3 parts][NBOARD*64 + 1 rows][F + 8 bf16]. Row NBOARD*64 stays zero: the
-// off-board taps of the 3x3 conv read it (no halo, no select). A row is F + 8 bf16 = an odd
-// number S of 16-byte slots. A ds_read_b128 is serviced in the lane groups {0-3,12-15,20-27},
-// {4-11,16-19,28-31} (+32 for the other half); here a half-wave reads 32 consecutive pixels at
-// one k-offset, so each group holds 16 pixels covering all residues mod 16 and slot(px) =
-// S*px mod 16 is distinct inside the group: conflict-free.
-// GEMM per conv layer, computed transposed (D = W X^T) on v_mfma_f32_32x32x16_bf16: M = F output
-// channels (32-channel tiles), N = NBOARD*64 pixels (32-pixel tiles), K = 9 taps x F (16-channel
-// k-steps). 8 waves, one 32x32 output tile each (F=64: 2 channel x 4 pixel tiles over 2 boards;
-// F=128: 4 x 2 over 1 board); per k-step a wave reads 3 activation fragments (LDS), loads 3
-// weight fragments (L2, prefetched two k-steps ahead) and issues 6 MFMAs (192 cycles), which
-// leaves most of each MFMA's issue gap free for the loads.
-// Lane maps: A lane l = out-channel l&31, in-channels 8(l>>5)..+7 (weights); B lane l = pixel
-// l&31, in-channels 8(l>>5)..+7 (activations); D col = l&31 = pixel, row = (reg&3) + 8(reg>>2) +
-// 4(l>>5) = out-channel: a lane ends with 4 runs of 4 consecutive channels of one pixel, stored
-// with 8-byte writes.
-// Split weights (rvz_resnet_split_weights): frag[layer][tap][kstep][part][ctile][lane][8] bf16,
-// so one wave's fragment is 1 KiB contiguous (one coalesced global_load_dwordx4 per lane).
-
-#ifdef RVZ_PHASE_TIMING   // tools/phase_timing.py: per-workgroup s_memtime at phase boundaries
-__device__ uint64_t g_phase[65536][8];
-__device__ uint64_t g_rt[65536][2];   // s_memrealtime (100 MHz) at start / end
-__device__ uint64_t g_wave[65536][16];
-#define PHASE(i) \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
-#define RT(i) \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) g_rt[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
-__device__ uint64_t g_stem[65536][8];
-__device__ uint32_t g_hwid[65536][2];   // HW_ID (CU, SE, ...), XCC_ID of each workgroup
-#define HWID() \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) { \
-        g_hwid[blockIdx.x][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4); \
-        g_hwid[blockIdx.x][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
-    }
-#define STEM_T(i) \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) g_stem[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
-#define WAVE_T(i) \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 65536) \
-        g_wave[blockIdx.x][(threadIdx.x >> 6) + 8 * (i)] = __builtin_amdgcn_s_memtime()
-#else
-#define PHASE(i)
-#define HWID()
-#define STEM_T(i)
-#define WAVE_T(i)
-#define RT(i)
-#endif
-
-// MFMA shape traits (D = W X^T: TM output channels x TN pixels, K input channels per step)
-struct Shape32 {   // v_mfma_f32_32x32x16_bf16 (RVZ_SPLIT_SHAPE=32)
-    [[maybe_unused]] static constexpr int TM = 32, TN = 32, K = 16, NG = 4;
-    typedef f32x16 acc_t;
-    // channel offset (within the tile) of register group g; registers 4g .. 4g+3
-    static __device__ __forceinline__ int chan(int g, int lane) { return 8 * g + 4 * (lane >> 5); }
-    static __device__ __forceinline__ acc_t mfma(bf16x8 a, bf16x8 b, acc_t c) {
-        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-    }
-};
-struct Shape16 {   // v_mfma_f32_16x16x32_bf16
-    static constexpr int TM = 16, TN = 16, K = 32, NG = 1;
-    typedef f32x4 acc_t;
-    static __device__ __forceinline__ int chan(int, int lane) { return 4 * (lane >> 4); }
-    static __device__ __forceinline__ acc_t mfma(bf16x8 a, bf16x8 b, acc_t c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-    }
-};
-
-// 16x16x32 by default: on random data the chip holds a higher clock on it than on 32x32x16
-// (MI355X_MICROARCH.md 'DVFS give-back' item 7); measured 0.875 vs 0.942 ms per C2 leaf batch
-#ifndef RVZ_SPLIT_SHAPE
-#define RVZ_SPLIT_SHAPE 16
-#endif
-#if RVZ_SPLIT_SHAPE == 16
-typedef Shape16 SplitShape;
-#ifndef RVZ_SPLIT_CTW
-#define RVZ_SPLIT_CTW 2      // channel tiles per wave
-#define RVZ_SPLIT_PTW 4      // pixel tiles per wave
-#endif
-#else
-typedef Shape32 SplitShape;
-#ifndef RVZ_SPLIT_CTW
-#define RVZ_SPLIT_CTW 1
-#define RVZ_SPLIT_PTW 2
-#endif
-#endif
-
-template <class S, int F, int NBOARD>
-struct CfgS {
-    // a row is F + PAD bf16 = R 16-byte slots. ds_read_b128 lane groups are {0-3,12-15,20-27},
-    // {4-11,16-19,28-31} (+32). 32x32x16: a half-wave reads 32 consecutive pixels at one
-    // k-offset, every group holds all 16 pixel residues mod 16 -> R odd is conflict-free.
-    // 16x16x32: a group holds pixels {0-3,12-15} at k-offset q and {4-11} at q+1 -> R = 2 mod 4.
-    static constexpr int CSB = S::TM == 32 ? F + 8 : F + 16;   // bf16 per pixel row
-    static constexpr int ZROW = NBOARD * 64;         // the zero row
-    static constexpr int PLANE = (ZROW + 1) * CSB;   // bf16 per part
-    static constexpr int ACT = 3 * PLANE;            // bf16 per buffer
-    static constexpr int XIN = NBOARD * 100 * 4;     // floats
-    static constexpr int BYTES = 2 * ACT * 2 + 4 * XIN;
-    static constexpr int KS = F / S::K;              // k-steps per tap
-    static constexpr int NIT = 9 * KS;               // k-steps per layer
-    static constexpr int CT = F / S::TM;             // channel tiles
-    static_assert(S::TM == 32 ? (CSB * 2 / 16) % 2 == 1 : (CSB * 2 / 16) % 4 == 2,
-                  "conflict-free row stride");
-    static_assert((PLANE * 2) % 16 == 0, "16-byte aligned parts");
-    static_assert(BYTES <= 160 * 1024, "fits the 160 KiB LDS of a CU");
-};
-
-#ifndef RVZ_SPLIT_PD
-#define RVZ_SPLIT_PD 3       // weight prefetch distance, k-steps
-#endif
-#ifndef RVZ_SPLIT_INTERLEAVE
-#define RVZ_SPLIT_INTERLEAVE 1   // loads placed between the MFMAs of a k-step
-#endif
-#define RVZ_SPLIT_PAD 4      // k-steps of padding after the last layer's weights (>= PD)
-static_assert(RVZ_SPLIT_PD <= RVZ_SPLIT_PAD, "prefetch stays inside the padded buffer");
-
-__host__ __device__ inline int64_t split_layer_elems(int F) { return (int64_t)9 * F * F * 3; }
-__host__ __device__ inline int64_t split_kstep_elems(int F) {   // one k-step, all parts/tiles
-    return (int64_t)3 * F * SplitShape::K;
-}
-
-// the wave's tiles: CTW channel tiles x PTW pixel tiles
-template <class S, int F, int CTW, int PTW>
-struct WaveTiles {
-    static constexpr int CG = F / (CTW * S::TM);     // channel groups (waves along channels)
-    int ct0, px[PTW];
-    __device__ WaveTiles(int wave, int lane) {
-        ct0 = (wave % CG) * CTW;
-        const int pt0 = (wave / CG) * PTW;
-#pragma unroll
-        for (int u = 0; u < PTW; ++u) px[u] = (pt0 + u) * S::TN + lane % S::TN;
-    }
-};
-
-// conv epilogue: bias (+ skip), ReLU, exact split back into the three parts; per register group
-// g of tile (c, u) the lane holds 4 consecutive channels of its pixel -> 8-byte writes. The skip
-// input of a residual block is the block input, which this lane itself produced (same tile map
-// in the stem and every conv): it stays in registers (res, fp32 — the exact value its split
-// encodes), RES adds it, KEEP stores the result as the next block's skip input.
-template <class S, int CTW, int PTW, bool REGRES>
-struct EpiRegs {
-    f32x4 bias[CTW][S::NG];
-    float res[CTW][PTW][REGRES ? S::NG * 4 : 1];
-};
-// skip input in registers where they fit (F = 64); at F = 128 they would spill, and the epilogue
-// re-reads it from LDS (joining its split)
-template <int F>
-struct RegRes {
-    static constexpr bool value = F <= 64;
-};
-
-template <class S, int F, int NBOARD, int CTW, int PTW, bool RES, bool KEEP>
-__device__ __forceinline__ void epilogue_split(uint16_t* __restrict__ out,
-                                               const typename S::acc_t (&hi)[CTW][PTW],
-                                               const typename S::acc_t (&lo)[CTW][PTW],
-                                               EpiRegs<S, CTW, PTW, RegRes<F>::value>& er,
-                                               const WaveTiles<S, F, CTW, PTW>& wt, int lane) {
-    using C = CfgS<S, F, NBOARD>;
-    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int c = 0; c < CTW; ++c)
-#pragma unroll
-        for (int u = 0; u < PTW; ++u)
-#pragma unroll
-            for (int g = 0; g < S::NG; ++g) {
-                const int n0 = (wt.ct0 + c) * S::TM + S::chan(g, lane);
-                uint16_t* o = out + wt.px[u] * C::CSB + n0;
-                constexpr bool REG = RegRes<F>::value;
-                typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
-                u16x4 s0, s1, s2;
-                if (RES && !REG) {
-                    s0 = *reinterpret_cast<const u16x4*>(o);
-                    s1 = *reinterpret_cast<const u16x4*>(o + C::PLANE);
-                    s2 = *reinterpret_cast<const u16x4*>(o + 2 * C::PLANE);
-                }
-                u32x2 d0, d1, d2;
-#pragma unroll
-                for (int hf = 0; hf < 2; ++hf) {
-                    f32x2 v;
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        const int j = 2 * hf + e, reg = 4 * g + j;
-                        v[e] = (hi[c][u][reg] + lo[c][u][reg]) + er.bias[c][g][j];
-                        if (RES) {                              // skip input
-                            if constexpr (REG) v[e] += er.res[c][u][reg];
-                            else v[e] += join3(s0[j], s1[j], s2[j]);
-                        }
-                        v[e] = fmaxf(v[e], 0.0f);
-                        if constexpr (KEEP && REG) er.res[c][u][reg] = v[e];
-                    }
-                    uint32_t h0, h1, h2;
-                    split3x2(v, h0, h1, h2);
-                    d0[hf] = h0;
-                    d1[hf] = h1;
-                    d2[hf] = h2;
-                }
-                *reinterpret_cast<u32x2*>(o) = d0;
-                *reinterpret_cast<u32x2*>(o + C::PLANE) = d1;
-                *reinterpret_cast<u32x2*>(o + 2 * C::PLANE) = d2;
-            }
-}
-
-template <class S, int F, int CTW, int PTW>
-__device__ __forceinline__ void load_bias(EpiRegs<S, CTW, PTW, RegRes<F>::value>& er, const float* __restrict__ bias,
-                                          const WaveTiles<S, F, CTW, PTW>& wt, int lane) {
-#pragma unroll
-    for (int c = 0; c < CTW; ++c)
-#pragma unroll
-        for (int g = 0; g < S::NG; ++g)
-            er.bias[c][g] = *reinterpret_cast<const f32x4*>(bias + (wt.ct0 + c) * S::TM +
-                                                            S::chan(g, lane));
-}
-
-// 8 bf16 parts p of 8 fp32 values
-__device__ __forceinline__ void split8(const float (&v)[8], bf16x8 (&out)[3]) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 w0, w1, w2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t a, b, c;
-        split3x2(f32x2{v[2 * i], v[2 * i + 1]}, a, b, c);
-        w0[i] = a;
-        w1[i] = b;
-        w2[i] = c;
-    }
-    out[0] = __builtin_bit_cast(bf16x8, w0);
-    out[1] = __builtin_bit_cast(bf16x8, w1);
-    out[2] = __builtin_bit_cast(bf16x8, w2);
-}
-
-// the six partial products: (weight part, activation part), hi first
-__device__ constexpr int kTW[6] = {0, 0, 2, 1, 0, 1};
-__device__ constexpr int kTA[6] = {0, 2, 0, 1, 1, 0};
-
-// stem conv 3 -> F (network.py:33-34 + BN folded) as a K = 27 (padded to 32) GEMM on the same
-// split MFMA and tile map as the trunk: k = tap*3 + ch; A = stem weights (split in registers),
-// B = the input taps read from the halo-padded xin; epilogue into actA.
-template <class S, int F, int NBOARD, int CTW, int PTW>
-__device__ __forceinline__ void stem_split(const float* xin, uint16_t* __restrict__ out,
-                                           const float* __restrict__ prm, const Layout& L,
-                                           int wave, int lane,
-                                           EpiRegs<S, CTW, PTW, RegRes<F>::value>& er) {
-    const WaveTiles<S, F, CTW, PTW> wt(wave, lane);
-    load_bias(er, prm + L.stem_b, wt, lane);
-    const int kq = 8 * (lane / S::TM);               // this lane's k offset in a step
-    typename S::acc_t hi[CTW][PTW], lo[CTW][PTW];
-#pragma unroll
-    for (int c = 0; c < CTW; ++c)
-#pragma unroll
-        for (int u = 0; u < PTW; ++u) {
-            hi[c][u] = typename S::acc_t{};
-            lo[c][u] = typename S::acc_t{};
-        }
-#pragma unroll
-    for (int ks = 0; ks < 32 / S::K; ++ks) {
-        bf16x8 wq[CTW][3], aq[PTW][3];
-#pragma unroll
-        for (int c = 0; c < CTW; ++c) {
-            const float* wrow = prm + L.stem_w + ((wt.ct0 + c) * S::TM + lane % S::TM) * 27;
-            float wv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = ks * S::K + kq + j;
-                wv[j] = k < 27 ? wrow[k] : 0.0f;
-            }
-            split8(wv, wq[c]);
-        }
-#pragma unroll
-        for (int u = 0; u < PTW; ++u) {
-            const int px = wt.px[u], b = px >> 6, r = (px & 63) >> 3, cc = px & 7;
-            float xv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int k = ks * S::K + kq + j, t = k / 3, ch = k % 3;
-                xv[j] = k < 27 ? xin[(b * 100 + (r + t / 3) * 10 + (cc + t % 3)) * 4 + ch] : 0.0f;
-            }
-            split8(xv, aq[u]);
-        }
-#pragma unroll
-        for (int term = 0; term < 6; ++term)
-#pragma unroll
-            for (int c = 0; c < CTW; ++c)
-#pragma unroll
-                for (int u = 0; u < PTW; ++u) {
-                    auto& acc = term == 0 ? hi[c][u] : lo[c][u];
-                    acc = S::mfma(wq[c][kTW[term]], aq[u][kTA[term]], acc);
-                }
-    }
-    epilogue_split<S, F, NBOARD, CTW, PTW, false, true>(out, hi, lo, er, wt, lane);
-}
-
-// sched_group_barrier pattern: NM MFMAs, the first ND gaps get one LDS read, the next NV one
-// global load
-template <int I, int NM, int ND, int NV>
-__device__ __forceinline__ void interleave_loads() {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if constexpr (I < ND) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    else if constexpr (I < ND + NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-    if constexpr (I + 1 < NM) interleave_loads<I + 1, NM, ND, NV>();
-}
-
-template <class S, int F, int NBOARD, int CTW, int PTW, bool RES, int BS = 8>
-__device__ __forceinline__ void conv_split(const uint16_t* __restrict__ in,
-                                           uint16_t* __restrict__ out,
-                                           const uint16_t* __restrict__ wl,   // layer fragments
-                                           const float* __restrict__ bias, int wave, int lane,
-                                           bf16x8 (&bc)[RVZ_SPLIT_PD][CTW][3],
-                                           EpiRegs<S, CTW, PTW, RegRes<F>::value>& er,
-                                           int ptag = -1) {
-    using C = CfgS<S, F, NBOARD>;
-    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_SPLIT_PD;
-    const WaveTiles<S, F, CTW, PTW> wt(wave, lane);
-    load_bias(er, bias, wt, lane);                  // lands during the k-loop
-    const int kq = 8 * (lane / S::TM);
-    // the taps of each of the lane's pixels that stay on its board
-    unsigned pmask[PTW];
-#pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-        const int rr = (wt.px[u] & 63) >> 3, cc = wt.px[u] & 7;
-        unsigned msk = 0;
-#pragma unroll
-        for (int t = 0; t < 9; ++t)
-            if ((unsigned)(rr + t / 3 - 1) < (unsigned)BS && (unsigned)(cc + t % 3 - 1) < (unsigned)BS)
-                msk |= 1u << t;
-        pmask[u] = msk;
-    }
-    typename S::acc_t hi[CTW][PTW], lo[CTW][PTW];
-#pragma unroll
-    for (int c = 0; c < CTW; ++c)
-#pragma unroll
-        for (int u = 0; u < PTW; ++u) {
-            hi[c][u] = typename S::acc_t{};
-            lo[c][u] = typename S::acc_t{};
-        }
-    // fragment (it, part, ctile) of this lane: wf[((it*3 + part)*CT + ctile)*64]
-    const bf16x8* wf = reinterpret_cast<const bf16x8*>(wl) + wt.ct0 * 64 + lane;
-    auto load_b = [&](bf16x8 (&bq)[CTW][3], int it) {
-#pragma unroll
-        for (int c = 0; c < CTW; ++c)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bq[c][p] = wf[((it * 3 + p) * CT + c) * 64];
-    };
-    auto load_a = [&](bf16x8 (&aq)[PTW][3], int it) {
-        const int t = it / KS, ks = it - t * KS;
-        const int off = (t / 3 - 1) * 8 + (t % 3 - 1);
-#pragma unroll
-        for (int u = 0; u < PTW; ++u) {
-            const int row = (pmask[u] >> t) & 1u ? wt.px[u] + off : C::ZROW;
-            const uint16_t* ap = in + row * C::CSB + ks * S::K + kq;
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-                aq[u][p] = *reinterpret_cast<const bf16x8*>(ap + p * C::PLANE);
-        }
-    };
-    // consecutive MFMAs of one wave go to different accumulators
-    auto compute = [&](const bf16x8 (&aq)[PTW][3], const bf16x8 (&bq)[CTW][3]) {
-#pragma unroll
-        for (int term = 0; term < 6; ++term)
-#pragma unroll
-            for (int c = 0; c < CTW; ++c)
-#pragma unroll
-                for (int u = 0; u < PTW; ++u) {
-                    auto& acc = term == 0 ? hi[c][u] : lo[c][u];
-                    acc = S::mfma(bq[c][kTW[term]], aq[u][kTA[term]], acc);
-                }
-    };
-    // Software pipeline, fully unrolled (constant register indices, no copies of in-flight
-    // loads): step it computes while step it+APD's activation fragments (LDS) and step it+PD's
-    // weight fragments (L2) load, one load per MFMA issue gap (an MFMA leaves most of its issue
-    // cycles free; 9+ loads back to back would let the matrix pipe drain). bc carries the next
-    // layer's first PD k-steps (layers are contiguous; the buffer has RVZ_SPLIT_PAD k-steps of
-    // padding after the last).
-    // activation prefetch distance: 2 k-steps where the registers allow (F = 64), else 1
-    constexpr int APD = F <= 64 ? 2 : 1;
-    bf16x8 bq[NIT + PD][CTW][3];
-    bf16x8 aq[APD + 1][PTW][3];
-#pragma unroll
-    for (int d = 0; d < PD; ++d)
-#pragma unroll
-        for (int c = 0; c < CTW; ++c)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bq[d][c][p] = bc[d][c][p];
-#pragma unroll
-    for (int d = 0; d < APD; ++d) load_a(aq[d], d);
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-        if (it + APD < NIT) load_a(aq[(it + APD) % (APD + 1)], it + APD);
-        load_b(bq[it + PD], it + PD);
-#if RVZ_SPLIT_INTERLEAVE
-        compute(aq[it % (APD + 1)], bq[it]);
-        interleave_loads<0, 6 * CTW * PTW, 3 * PTW, 3 * CTW>();
-        __builtin_amdgcn_sched_barrier(0);
-#else
-        __builtin_amdgcn_sched_barrier(0);
-        compute(aq[it % (APD + 1)], bq[it]);
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-    }
-#pragma unroll
-    for (int d = 0; d < PD; ++d)
-#pragma unroll
-        for (int c = 0; c < CTW; ++c)
-#pragma unroll
-            for (int p = 0; p < 3; ++p) bc[d][c][p] = bq[NIT + d][c][p];
-    if (ptag >= 0) {
-        PHASE(ptag);
-        WAVE_T(0);
-    }
-    // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
-    epilogue_split<S, F, NBOARD, CTW, PTW, RES, RES>(out, hi, lo, er, wt, lane);
-}
-
-// one workgroup = 4 waves (one per SIMD) = NBOARD boards; wave tile CTW x PTW MFMA tiles
-template <class S, int F, int NBOARD, int CTW, int PTW, int BS>
-__global__ __launch_bounds__(256, 1) void k_resnet_split(const float* __restrict__ x,
-                                                         int n_boards,
-                                                         const float* __restrict__ prm, Layout L,
-                                                         const uint16_t* __restrict__ wsp,
-                                                         int n_blocks, float* __restrict__ work) {
-    using C = CfgS<S, F, NBOARD>;
-    using WT = WaveTiles<S, F, CTW, PTW>;
-    static_assert(WT::CG * (NBOARD * 64 / (PTW * S::TN)) == 4, "4 waves");
-    constexpr int NTHR = 256;
-    __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
-    uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
-    uint16_t* actB = actA + C::ACT;
-    float* xin = reinterpret_cast<float*>(actB + C::ACT);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g0 = blockIdx.x * NBOARD;
-    PHASE(0);
-    RT(0);
-
-    // zero rows of both buffers, all parts (6 consecutive planes)
-    for (int i = tid; i < 6 * C::CSB; i += NTHR) {
-        const int part = i / C::CSB, k = i % C::CSB;
-        actA[part * C::PLANE + C::ZROW * C::CSB + k] = 0;
-    }
-    // the first PD k-steps' weight fragments, in flight during the input and stem
-    bf16x8 bc[RVZ_SPLIT_PD][CTW][3];
-    if (n_blocks > 0) {
-        const bf16x8* wf = reinterpret_cast<const bf16x8*>(wsp) + WT(wave, lane).ct0 * 64 + lane;
-#pragma unroll
-        for (int s = 0; s < RVZ_SPLIT_PD; ++s)
-#pragma unroll
-            for (int c = 0; c < CTW; ++c)
-#pragma unroll
-                for (int p = 0; p < 3; ++p) bc[s][c][p] = wf[((s * 3 + p) * C::CT + c) * 64];
-    }
-    load_input<NBOARD, BS>(x, n_boards, g0, xin, tid, NTHR);
-    __syncthreads();
-    const ActSplit outA{actA, C::CSB, C::PLANE};
-    EpiRegs<S, CTW, PTW, RegRes<F>::value> er;      // bias and skip-input registers
-    stem_split<S, F, NBOARD, CTW, PTW>(xin, actA, prm, L, wave, lane, er);
-    __syncthreads();
-    PHASE(1);
-    const int64_t LW = split_layer_elems(F);
-    for (int blk = 0; blk < n_blocks; ++blk) {
-        const int l1 = 2 * blk, l2 = 2 * blk + 1;
-        conv_split<S, F, NBOARD, CTW, PTW, false, BS>(actA, actB, wsp + l1 * LW,
-                                                  prm + L.res_b + (size_t)l1 * F, wave, lane, bc,
-                                                  er, blk == 0 ? 4 : -1);
-        if (blk == 0) {
-            PHASE(5);
-            WAVE_T(1);
-        }
-        __syncthreads();
-        if (blk == 0) PHASE(6);
-        conv_split<S, F, NBOARD, CTW, PTW, true, BS>(actB, actA, wsp + l2 * LW,
-                                                 prm + L.res_b + (size_t)l2 * F, wave, lane, bc,
-                                                 er);
-        __syncthreads();
-    }
-    PHASE(2);
-    head_convs<F, NBOARD, NTHR, BS>(outA, reinterpret_cast<float*>(actB), prm, L,
-                                    HeadsGlobal{work, g0, n_boards}, tid);
-    PHASE(3);
-    RT(1);
-}
-
-// res_w[l][t][n][k] fp32 -> frag[l][t][ks][part][ctile][lane][8] bf16 parts, for SplitShape:
-// lane = ((k % K) / 8) * TM + n % TM (the A-operand lane map)
-__global__ void k_split_weights(const float* __restrict__ w, int F, int64_t total,
-                                uint16_t* __restrict__ out) {
-    constexpr int K = SplitShape::K, TM = SplitShape::TM;
-    const int KS = F / K, CT = F / TM;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int k = (int)(i % F), n = (int)((i / F) % F);
-        const int64_t lt = i / ((int64_t)F * F);             // layer*9 + tap
-        const int ks = k / K, j = k % 8, ct = n / TM;
-        const int ln = ((k % K) / 8) * TM + n % TM;
-        uint16_t h[3];
-        split3(w[i], h[0], h[1], h[2]);
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-            out[((((lt * KS + ks) * 3 + p) * CT + ct) * 64 + ln) * 8 + j] = h[p];
-    }
-}
 
 // =============================================================================================
 // h2 kernel: fp32 as an exact two-part f16 split, three partial products (rvz_resnet_fwd_h2)
@@ -1184,15 +60,22 @@ typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 #ifndef RVZ_H2_OCC
 #define RVZ_H2_OCC 2         // workgroups per CU the register budget is sized for
 #endif
-#define RVZ_H2_PAD 4
-static_assert(RVZ_H2_PD <= RVZ_H2_PAD, "prefetch stays inside the padded blob");
+#ifndef RVZ_H2_ILV
+#define RVZ_H2_ILV 1         // 8x8, 2 boards per workgroup: row-interleaved pixels, edge taps skipped
+#endif                       // (0: board-major pixels, every tap computed)
 
 constexpr int H2_K = 32, H2_TM = 16, H2_TN = 16;
 
 __host__ __device__ inline int64_t h2_layer_elems(int F) { return (int64_t)9 * F * F * 2; }
 __host__ __device__ inline int64_t h2_kstep_elems(int F) { return (int64_t)2 * F * H2_K; }
+// zero k-steps after the last layer: the weight prefetch of the next (absent) layer reads them.
+// (A mirrored wave (ILV) starts a layer at tap 8; its prefetch past the last layer lands in the
+// stem / scale words or past the blob, where the buffer descriptor's range check returns 0: the
+// values are discarded either way.)
+__host__ __device__ inline int64_t h2_pad_ksteps(int) { return 4; }
+static_assert(RVZ_H2_PD <= 4, "prefetch stays inside the padded blob");
 __host__ __device__ inline int64_t h2_stem_off(int F, int NB) {
-    return 2 * NB * h2_layer_elems(F) + RVZ_H2_PAD * h2_kstep_elems(F);
+    return 2 * NB * h2_layer_elems(F) + h2_pad_ksteps(F) * h2_kstep_elems(F);
 }
 __host__ __device__ inline int64_t h2_scale_off(int F, int NB) {   // uint16 units, 16-B aligned
     return h2_stem_off(F, NB) + (int64_t)2 * F * H2_K;
@@ -1218,14 +101,26 @@ __device__ __forceinline__ float h16f(uint16_t h) {
 // an embedding in the 8x8 grid), rounded up to whole 16-pixel MFMA tiles; rows past the boards
 // are padding (no valid tap, never read), up to a multiple of RND (whole pixel tiles for every
 // wave: 16 x the waves along the pixels).
-template <int NB, int BS, int RND>
+// ILV (two 8x8 boards): row-interleaved, px = r * 16 + b * 8 + c, so a 16-pixel tile is board
+// row r of both boards and the taps of row 0 (dr = -1) and row 7 (dr = +1) leave the boards for
+// the whole tile: those tile x tap products are skipped, 1/12 of the conv MFMAs (conv_h2).
+template <int NB, int BS, int RND, bool ILV = false>
 struct GeoH {
     static constexpr int PPB = BS * BS;
     static constexpr int NVALID = NB * PPB;
     static constexpr int NPIX = (NVALID + RND - 1) / RND * RND;
+    static constexpr int RS = ILV ? NB * BS : BS;    // pixel-row stride of a board row
+    static_assert(!ILV || (NB == 2 && BS == 8), "interleaved rows: two 8x8 boards");
+    static __device__ __forceinline__ int cell_of(int px) {
+        return ILV ? (px >> 4) * 8 + (px & 7) : px % PPB;
+    }
+    static __device__ __forceinline__ int board_of(int px) { return ILV ? (px >> 3) & 1 : px / PPB; }
+    static __device__ __forceinline__ int row_of(int b, int cell) {
+        return ILV ? (cell >> 3) * 16 + b * 8 + (cell & 7) : b * PPB + cell;
+    }
     // the 3x3 taps of pixel px that stay on its board (bit t = tap (t/3 - 1, t%3 - 1))
     static __device__ __forceinline__ unsigned taps(int px) {
-        const int cell = px % PPB, r = cell / BS, c = cell % BS;
+        const int cell = cell_of(px), r = cell / BS, c = cell % BS;
         unsigned m = 0;
 #pragma unroll
         for (int t = 0; t < 9; ++t)
@@ -1233,7 +128,7 @@ struct GeoH {
                 m |= 1u << t;
         return px < NVALID ? m : 0u;
     }
-    static __device__ __forceinline__ int tap_offset(int t) { return (t / 3 - 1) * BS + (t % 3 - 1); }
+    static __device__ __forceinline__ int tap_offset(int t) { return (t / 3 - 1) * RS + (t % 3 - 1); }
 };
 
 template <int F, int NPIX>
@@ -1268,17 +163,46 @@ struct ActH2 {
     }
 };
 
+// A wave's output tiles: CTW channel tiles from ct0 and PTW pixel tiles. ilv (GeoH ILV): pixel
+// group 0 holds board rows 0-3 (tile u = row u), group 1 rows 7-4 (tile u = row 7 - u), so tile 0
+// is the edge row of either group.
 template <int F, int CTW, int PTW>
 struct WaveTilesH {
     static constexpr int CG = F / (CTW * H2_TM);
     int ct0, px[PTW];
-    __device__ WaveTilesH(int wave, int lane) {
+    __device__ WaveTilesH(int wave, int lane, bool ilv = false) {
         ct0 = (wave % CG) * CTW;
-        const int pt0 = (wave / CG) * PTW;
+        const int pg = wave / CG, pt0 = pg * PTW;
 #pragma unroll
-        for (int u = 0; u < PTW; ++u) px[u] = (pt0 + u) * H2_TN + lane % H2_TN;
+        for (int u = 0; u < PTW; ++u)
+            px[u] = (ilv ? (pg ? 7 - u : u) : pt0 + u) * H2_TN + lane % H2_TN;
     }
 };
+
+// Weight fragments are read through a buffer descriptor over the whole blob: the wave-uniform
+// part of the address (layer, tap, k-step, part, channel tile) is the scalar soffset and the
+// lane's 16-byte slot the only VGPR, so a mirrored wave's runtime tap order costs scalar adds.
+// Reads past the blob return 0 (the descriptor's range check).
+struct H2W {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ H2W(const uint16_t* blob, int64_t elems)
+        : r(__builtin_amdgcn_make_buffer_rsrc((void*)blob, (short)0, (int)(elems * 2), 0x00020000)) {}
+    // f16x8 fragment at f16x8 index `idx` (wave-uniform) + this lane
+    __device__ __forceinline__ f16x8 load(int idx, int lane) const {
+        return __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16,
+                                                                               idx * 16, 0));
+    }
+};
+// f16x8 index of k-step `it` of a layer (it >= NIT: the next layer's) from the layer's base:
+// [tap][kstep][part][ctile][lane]. mirror: the wave walks the taps as 8 - t (ILV pixel group 1:
+// dr, dc -> -dr, -dc), so both groups meet their edge taps at the same it.
+template <int F>
+__device__ __forceinline__ int h2_frag(int it, bool mirror) {
+    constexpr int KS = F / H2_K, NIT = 9 * KS, CT = F / H2_TM, KSTEP = 2 * CT * 64;
+    const int lay = it / NIT, itn = it % NIT, t = itn / KS, ks = itn % KS;
+    const int tn = mirror ? 8 - t : t;
+    return (lay * NIT + tn * KS + ks) * KSTEP;
+}
 
 // RVZ_H2_SKIP_LDS 1: the skip input is re-read from LDS as its two parts (x0 + x1, 22 bits) at
 // the place conv B overwrites, instead of kept in 32 fp32 registers (frees them for a deeper
@@ -1356,7 +280,8 @@ __device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 // the three partial products, consecutive MFMAs on different accumulators
-template <int CTW, int PTW>
+// (U0 = 1: pixel tile 0 skipped, its tap is off the boards for the whole tile)
+template <int CTW, int PTW, int U0 = 0>
 __device__ __forceinline__ void mma3(f32x4 (&acc)[CTW][PTW], const f16x8 (&a)[PTW][2],
                                      const f16x8 (&w)[CTW][2]) {
 #pragma unroll
@@ -1364,7 +289,7 @@ __device__ __forceinline__ void mma3(f32x4 (&acc)[CTW][PTW], const f16x8 (&a)[PT
 #pragma unroll
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
-            for (int u = 0; u < PTW; ++u)
+            for (int u = U0; u < PTW; ++u)
                 acc[c][u] = mfma_h(w[c][t == 1 ? 1 : 0], a[u][t == 2 ? 1 : 0], acc[c][u]);
 }
 
@@ -1387,11 +312,11 @@ __device__ __forceinline__ void stem_h2_load(const uint16_t* __restrict__ blob,
 
 // the stem's operands are loaded up front (stem_h2_load, with the leaf planes): one global
 // round trip before the first MFMA instead of three dependent ones
-template <int F, int NBOARD, int CTW, int PTW, int BS>
+template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV>
 __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__ out,
                                         const f16x8 (&w)[CTW][2], int wave, int lane,
                                         EpiH<CTW, PTW>& er, bool& ovf) {
-    const WaveTilesH<F, CTW, PTW> wt(wave, lane);
+    const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
     // K order h2_stem_slot: this lane group's taps 2g, 2g + 1 and (groups 0, 1) part of tap 8
     const int kg = lane >> 4, ta = 2 * kg, tb = 2 * kg + 1;
     const int oa = (ta / 3) * 10 + ta % 3, ob = (tb / 3) * 10 + tb % 3;
@@ -1399,8 +324,9 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
     f16x8 a[PTW][2];
 #pragma unroll
     for (int u = 0; u < PTW; ++u) {
-        using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
-        const int px = wt.px[u], b = px / G::PPB, r = (px % G::PPB) / BS, cc = px % BS;
+        using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
+        const int px = wt.px[u], b = G::board_of(px), r = G::cell_of(px) / BS,
+                  cc = G::cell_of(px) % BS;
         const bool on = px < G::NVALID;               // padding rows: zero input
         const int at = b * 100 + r * 10 + cc;         // tap 0 of this pixel in the padded image
         const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -1437,42 +363,56 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 #endif
     }
     STEM_T(5);
-    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>::NPIX, CTW, PTW, false, true>(
+        out, acc, er, wt, lane, ovf);
 }
 
-template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS>
+template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
-                                        const uint16_t* __restrict__ wl,   // layer fragments
+                                        const H2W& wr, int wl,   // layer base, f16x8 units
                                         const float* __restrict__ bias,
                                         const float* __restrict__ isc, int wave, int lane,
                                         f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
                                         bool& ovf) {
-    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     using C = CfgH<F, G::NPIX>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
-    const WaveTilesH<F, CTW, PTW> wt(wave, lane);
+    // ILV: tile 0 is board row 0 (pixel group 0) or row 7 (group 1), and the taps with dr = -1
+    // (row 0) or dr = +1 (row 7) leave the boards for all its pixels. Group 1 walks the taps
+    // mirrored (8 - t), so both groups skip tile 0's A loads and MFMAs in k-steps [0, SKIP), a
+    // compile-time window. Measured (tools/ab_h2.py, one box, C2 trunk): -1.9%; the mirrored
+    // order alone costs +3.3% (the two waves of a channel group no longer fetch the same weight
+    // fragments together: more L2 traffic, a lower clock), the skip saves 5%. Instantiating the
+    // k-loop once per group instead (both in natural order) spilled 74 VGPRs.
+    constexpr int SKIP = ILV ? 3 * KS : 0;
+    const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
+    const bool mirror = ILV && wave / WaveTilesH<F, CTW, PTW>::CG != 0;
     load_epi(er, bias, isc, wt, lane);                // lands during the k-loop
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
-    unsigned pmask[PTW];
+    unsigned pmask[PTW];                              // valid taps in iteration order
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) pmask[u] = G::taps(wt.px[u]);
+    for (int u = 0; u < PTW; ++u) {
+        const unsigned m = G::taps(wt.px[u]);
+        pmask[u] = mirror ? __builtin_bitreverse32(m) >> 23 : m;
+    }
     f32x4 acc[CTW][PTW];
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
 #pragma unroll
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
-    const f16x8* wf = reinterpret_cast<const f16x8*>(wl) + wt.ct0 * 64 + lane;
+    const int wu = wl + wt.ct0 * 64;
     auto load_b = [&](f16x8 (&bq)[CTW][2], int it) {
+        const int f = wu + h2_frag<F>(it, mirror);
 #pragma unroll
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
-            for (int p = 0; p < 2; ++p) bq[c][p] = wf[((it * 2 + p) * CT + c) * 64];
+            for (int p = 0; p < 2; ++p) bq[c][p] = wr.load(f + (p * CT + c) * 64, lane);
     };
     auto load_a = [&](f16x8 (&aq)[PTW][2], int it) {
         const int t = it / KS, ks = it - t * KS;
-        const int off = G::tap_offset(t);
+        const int off = mirror ? -G::tap_offset(t) : G::tap_offset(t);
 #pragma unroll
-        for (int u = 0; u < PTW; ++u) {
+        for (int u = (it < SKIP ? 1 : 0); u < PTW; ++u) {
             const int nat = wt.px[u] + off;
             const int row = (pmask[u] >> t) & 1u ? nat : C::ZROW + (nat & 7);
             const uint16_t* ap = in + C::at(row, 0, kq) + ks * C::KSP;
@@ -1493,10 +433,17 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     for (int d = 0; d < APD; ++d) load_a(aq[d], d);
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-        if (it + APD < NIT) load_a(aq[(it + APD) % (APD + 1)], it + APD);
+        const int ia = it + APD;                      // the A operands loaded this k-step
+        if (ia < NIT) load_a(aq[ia % (APD + 1)], ia);
         load_b(bq[it + PD], it + PD);
-        mma3(acc, aq[it % (APD + 1)], bq[it]);
-        interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+        if (it < SKIP) {
+            mma3<CTW, PTW, 1>(acc, aq[it % (APD + 1)], bq[it]);
+            if (ia < SKIP) interleave_loads<0, 3 * CTW * (PTW - 1), 2 * (PTW - 1), 2 * CTW>();
+            else interleave_loads<0, 3 * CTW * (PTW - 1), 2 * PTW, 2 * CTW>();
+        } else {
+            mma3(acc, aq[it % (APD + 1)], bq[it]);
+            interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
@@ -1539,15 +486,16 @@ template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
-                 float* __restrict__ work, float* __restrict__ logits,
-                 float* __restrict__ value, const int32_t* __restrict__ n_live,
+                 float* __restrict__ work, const int32_t* __restrict__ n_live,
                  uint64_t* __restrict__ stamps, const uint32_t* __restrict__ stamp_ctr,
                  int ring) {
-    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F>;
-    using C = CfgH<F, G::NPIX>;
     using WT = WaveTilesH<F, CTW, PTW>;
+    // row-interleaved pair of 8x8 boards (GeoH ILV): two pixel groups of 4 tiles = 8 board rows
+    constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
+    using C = CfgH<F, G::NPIX>;
     static_assert(WT::CG * (G::NPIX / (PTW * H2_TN)) == 4, "4 waves");
-    static_assert((1024 + NBOARD * (192 + 256)) * 4 <= C::ACT * 2, "heads scratch fits in B");
+    static_assert(1024 * 4 <= C::ACT * 2, "head-conv partial sums fit in B");
     static_assert(NBOARD * 100 * 4 * 4 <= C::ACT * 2, "xin fits in buffer B");
     constexpr int NTHR = 256;
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
@@ -1586,15 +534,19 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         const int plane = i / (8 * H2_K), k = i % (8 * H2_K);
         actA[plane * C::KSP + C::ZROW * H2_K + k] = 0;
     }
+    const H2W wr(blob, h2_blob_elems(F, n_blocks));
     f16x8 bc[RVZ_H2_PD][CTW][2];
     if (n_blocks > 0) {
-        const f16x8* wf = reinterpret_cast<const f16x8*>(blob) + WT(wave, lane).ct0 * 64 + lane;
+        const int wu = WT(wave, lane).ct0 * 64;
+        const bool mirror = ILV && wave / WT::CG != 0;
 #pragma unroll
-        for (int s = 0; s < RVZ_H2_PD; ++s)
+        for (int s = 0; s < RVZ_H2_PD; ++s) {
+            const int f = wu + h2_frag<F>(s, mirror);
 #pragma unroll
             for (int c = 0; c < CTW; ++c)
 #pragma unroll
-                for (int p = 0; p < 2; ++p) bc[s][c][p] = wf[((s * 2 + p) * C::CT + c) * 64];
+                for (int p = 0; p < 2; ++p) bc[s][c][p] = wr.load(f + (p * C::CT + c) * 64, lane);
+        }
     }
     XinStage<NBOARD, BS, NTHR> st;
     st.load(x, n_boards, g0, tid);
@@ -1606,7 +558,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     STEM_T(1);
     __syncthreads();
     STEM_T(2);
-    stem_h2<F, NBOARD, CTW, PTW, BS>(xin, actA, ws, wave, lane, er, ovf);
+    stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
     STEM_T(3);
     __syncthreads();
     PHASE(1);
@@ -1614,31 +566,21 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
     for (int blk = 0; blk < n_blocks; ++blk) {
         const int l1 = 2 * blk, l2 = 2 * blk + 1;
-        conv_h2<F, NBOARD, CTW, PTW, false, BS>(actA, actB, blob + l1 * LW,
+        conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV>(actA, actB, wr, (int)(l1 * LW / 8),
                                                 prm + L.res_b + (size_t)l1 * F, isc + l1 * F,
                                                 wave, lane, bc, er, ovf);
         if (blk == 0) PHASE(5);
         __syncthreads();
         if (blk == 0) PHASE(6);
-        conv_h2<F, NBOARD, CTW, PTW, true, BS>(actB, actA, blob + l2 * LW,
+        conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV>(actB, actA, wr, (int)(l2 * LW / 8),
                                                prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
                                                wave, lane, bc, er, ovf);
         __syncthreads();
     }
     PHASE(2);
-    if (logits) {          // the FC heads in this kernel: hpv and the fc1 output in buffer B
-        float* part = reinterpret_cast<float*>(actB);
-        float* hpv = part + 1024;
-        float* h1 = hpv + NBOARD * 192;
-        head_convs<F, NBOARD, NTHR, BS, true>(ActH2<F, G::NPIX>{actA}, part, prm, L, HeadsLds{hpv},
-                                              tid);
-        __syncthreads();
-        head_fcs<NBOARD, NTHR, BS>(hpv, h1, prm, L, g0, n_boards, logits, value, tid);
-    } else {
-        head_convs<F, NBOARD, NTHR, BS, true>(ActH2<F, G::NPIX>{actA},
-                                              reinterpret_cast<float*>(actB), prm, L,
-                                              HeadsGlobal{work, g0, n_boards}, tid);
-    }
+    // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
+    head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA}, reinterpret_cast<float*>(actB),
+                                          prm, L, HeadsGlobal{work, g0, n_boards}, tid);
     PHASE(3);
     RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
@@ -1714,21 +656,7 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
         blob[(((base + 1) * CT + ct) * 64 + ln) * 8 + k % 8] = __builtin_bit_cast(uint16_t, h1);
     }
 }
-
 }  // namespace
-
-template <int BS>
-static void launch_trunk(const float* x, int32_t n, const float* params, const uint16_t* wsplit,
-                         int32_t filters, int32_t blocks, float* work, hipStream_t s) {
-    const Layout L = make_layout(filters, blocks, BS);
-    if (filters == 64)
-        hipLaunchKernelGGL((k_resnet_split<SplitShape, 64, 2, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW, BS>),
-                           dim3((n + 1) / 2), dim3(256), 0, s, x, n, params, L, wsplit, blocks,
-                           work);
-    else
-        hipLaunchKernelGGL((k_resnet_split<SplitShape, 128, 1, RVZ_SPLIT_CTW, RVZ_SPLIT_PTW, BS>),
-                           dim3(n), dim3(256), 0, s, x, n, params, L, wsplit, blocks, work);
-}
 
 // workgroups of one h2 trunk launch (k_resnet_h2's grid)
 static int h2_grid(int bs, int filters, int n) {
@@ -1738,10 +666,9 @@ static int h2_grid(int bs, int filters, int n) {
 
 template <int BS>
 static void launch_trunk_h2(const float* x, int32_t n, const float* params, const uint16_t* blob,
-                            int32_t filters, int32_t blocks, float* work, float* logits,
-                            float* value, hipStream_t s, const int32_t* n_live = nullptr,
-                            uint64_t* stamps = nullptr, const uint32_t* stamp_ctr = nullptr,
-                            int ring = 1) {
+                            int32_t filters, int32_t blocks, float* work, hipStream_t s,
+                            const int32_t* n_live, uint64_t* stamps, const uint32_t* stamp_ctr,
+                            int ring) {
     const Layout L = make_layout(filters, blocks, BS);
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
@@ -1749,17 +676,16 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
     if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
         if (filters == 64)
             hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), dim3((n + 3) / 4), dim3(256), 0, s,
-                               x, n, params, L, blob, blocks, work, logits, value, n_live, stamps, stamp_ctr, ring);
+                               x, n, params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
         else
             hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), dim3(n), dim3(256), 0, s, x, n,
-                               params, L, blob, blocks, work, logits, value, n_live, stamps, stamp_ctr, ring);
+                               params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
     } else if (filters == 64)
         hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), dim3((n + 1) / 2), dim3(256),
-                           RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, logits, value,
-                           n_live, stamps, stamp_ctr, ring);
+                           RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
     else
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), dim3(n), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work, logits, value, n_live, stamps, stamp_ctr, ring);
+                           params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
 }
 
 extern "C" {
@@ -1770,30 +696,6 @@ int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks) {
     if ((filters != 64 && filters != 128) || blocks < 0 || !board_ok(board)) return RVZ_EINVAL;
     return make_layout(filters, blocks, board).total;
 }
-
-int rvz_resnet_fwd_f32(int32_t board, const float* x, int32_t n, const float* params,
-                       int32_t filters, int32_t blocks, float* logits, float* value,
-                       void* stream) {
-    if (board != 8 || !x || !params || !logits || !value || n < 0 || blocks < 0)
-        return RVZ_EINVAL;
-    if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
-    if (n == 0) return RVZ_OK;
-    const Layout L = make_layout(filters, blocks);
-    hipStream_t s = (hipStream_t)stream;
-    if (filters == 64) {
-        dim3 grid((n + 1) / 2), block(256);
-        hipLaunchKernelGGL((k_resnet_fwd<64, 2>), grid, block, 0, s, x, n, params, L, blocks,
-                           logits, value);
-    } else if (filters == 128) {
-        dim3 grid(n), block(256);
-        hipLaunchKernelGGL((k_resnet_fwd<128, 1>), grid, block, 0, s, x, n, params, L, blocks,
-                           logits, value);
-    } else {
-        return RVZ_EINVAL;
-    }
-    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
-}
-
 #ifdef RVZ_PHASE_TIMING
 int rvz_hwid_read(uint32_t* host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hwid), (size_t)n * 2 * sizeof(uint32_t)) ==
@@ -1816,44 +718,8 @@ int rvz_phase_read(uint64_t* host, int n) {
                    hipSuccess ? 0 : -5;
 }
 #endif
-
-int64_t rvz_resnet_split_size(int32_t filters, int32_t blocks) {
-    if ((filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
-    // + padding: the last layer's weight prefetch runs up to RVZ_SPLIT_PAD steps past the end
-    return (int64_t)2 * blocks * split_layer_elems(filters) +
-           RVZ_SPLIT_PAD * split_kstep_elems(filters);
-}
-
-int rvz_resnet_split_weights(const float* params, int32_t filters, int32_t blocks, uint16_t* out,
-                             void* stream) {
-    if (!params || (!out && blocks > 0) || (filters != 64 && filters != 128) || blocks < 0)
-        return RVZ_EINVAL;
-    if (blocks == 0) return RVZ_OK;
-    const Layout L = make_layout(filters, blocks);
-    const int64_t total = (int64_t)2 * blocks * 9 * filters * filters;
-    const int64_t nblk = (total + 255) / 256;
-    hipLaunchKernelGGL(k_split_weights, dim3((unsigned)(nblk < 4096 ? nblk : 4096)), dim3(256), 0,
-                       (hipStream_t)stream, params + L.res_w, filters, total, out);
-    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
-}
-
 // + 4 floats: word n*192 is the h2 kernel's sticky activation-overflow flag
 int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192 + 4; }
-
-int rvz_resnet_trunk_split(int32_t board, const float* x, int32_t n, const float* params,
-                           const uint16_t* wsplit, int32_t filters, int32_t blocks, float* work,
-                           void* stream) {
-    if (!x || !params || (!wsplit && blocks > 0) || !work || n < 0 || blocks < 0 ||
-        !board_ok(board) || (filters != 64 && filters != 128))
-        return RVZ_EINVAL;
-    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)wsplit & 15) != 0) return RVZ_EINVAL;
-    if (n == 0) return RVZ_OK;
-    hipStream_t s = (hipStream_t)stream;
-    if (board == 8) launch_trunk<8>(x, n, params, wsplit, filters, blocks, work, s);
-    else launch_trunk<6>(x, n, params, wsplit, filters, blocks, work, s);
-    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
-}
-
 int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const float* params,
                            int32_t filters, int32_t blocks, float* logits, float* value,
                            const int32_t* n_live, uint32_t* stamp_ctr, void* stream) {
@@ -1863,25 +729,12 @@ int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const fl
     if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     const Layout L = make_layout(filters, blocks, board);
-#ifndef RVZ_HEADS_MFMA
-#define RVZ_HEADS_MFMA 1
-#endif
-    if (RVZ_HEADS_MFMA) {
-        const dim3 grid((n + 15) / 16), block(256);
-        if (board == 8)
-            hipLaunchKernelGGL(k_heads_mfma<8>, grid, block, 0, (hipStream_t)stream, work, n,
-                               params, L, logits, value, n_live, stamp_ctr);
-        else
-            hipLaunchKernelGGL(k_heads_mfma<6>, grid, block, 0, (hipStream_t)stream, work, n,
-                               params, L, logits, value, n_live, stamp_ctr);
-        return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
-    }
-    const dim3 grid((n + FCB - 1) / FCB), block(256);
+    const dim3 grid((n + 15) / 16), block(256);
     if (board == 8)
-        hipLaunchKernelGGL(k_heads_fc<8>, grid, block, 0, (hipStream_t)stream, work, n, params,
+        hipLaunchKernelGGL(k_heads_mfma<8>, grid, block, 0, (hipStream_t)stream, work, n, params,
                            L, logits, value, n_live, stamp_ctr);
     else
-        hipLaunchKernelGGL(k_heads_fc<6>, grid, block, 0, (hipStream_t)stream, work, n, params,
+        hipLaunchKernelGGL(k_heads_mfma<6>, grid, block, 0, (hipStream_t)stream, work, n, params,
                            L, logits, value, n_live, stamp_ctr);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
@@ -1892,17 +745,6 @@ int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float
     return rvz_resnet_heads_fc_ex(board, work, n, params, filters, blocks, logits, value, nullptr,
                                   nullptr, stream);
 }
-
-int rvz_resnet_fwd_split(int32_t board, const float* x, int32_t n, const float* params,
-                         const uint16_t* wsplit, int32_t filters, int32_t blocks, float* work,
-                         float* logits, float* value, void* stream) {
-    if (!logits || !value) return RVZ_EINVAL;
-    const int rc =
-        rvz_resnet_trunk_split(board, x, n, params, wsplit, filters, blocks, work, stream);
-    if (rc != RVZ_OK) return rc;
-    return rvz_resnet_heads_fc(board, work, n, params, filters, blocks, logits, value, stream);
-}
-
 int64_t rvz_resnet_h2_size(int32_t filters, int32_t blocks) {
     if ((filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
     return h2_blob_elems(filters, blocks);
@@ -1916,7 +758,7 @@ int rvz_resnet_h2_weights(const float* params, int32_t filters, int32_t blocks, 
     const Layout L = make_layout(filters, blocks);
     // the prefetch padding after the last layer reads zeros
     if (hipMemsetAsync(blob + 2 * blocks * h2_layer_elems(filters), 0,
-                       RVZ_H2_PAD * h2_kstep_elems(filters) * 2, s) != hipSuccess)
+                       h2_pad_ksteps(filters) * h2_kstep_elems(filters) * 2, s) != hipSuccess)
         return RVZ_EHIP;
     hipLaunchKernelGGL(k_h2_weights, dim3(filters, 1 + 2 * blocks), dim3(64), 0, s, params, L,
                        (int)filters, (int)blocks, blob);
@@ -1934,10 +776,10 @@ int rvz_resnet_trunk_h2_ex(int32_t board, const float* x, int32_t n, const float
     if (n == 0) return RVZ_OK;
     hipStream_t s = (hipStream_t)stream;
     if (board == 8)
-        launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, n_live,
+        launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, s, n_live,
                            stamps, stamp_ctr, ring > 0 ? ring : 1);
     else
-        launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, nullptr, nullptr, s, n_live,
+        launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, s, n_live,
                            stamps, stamp_ctr, ring > 0 ? ring : 1);
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
@@ -1958,22 +800,6 @@ int rvz_resnet_fwd_h2_ex(int32_t board, const float* x, int32_t n, const float* 
                          const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
                          float* logits, float* value, const int32_t* n_live, void* stream) {
     if (!logits || !value) return RVZ_EINVAL;
-#ifndef RVZ_H2_FC_IN
-#define RVZ_H2_FC_IN 0
-#endif
-    if (RVZ_H2_FC_IN) {     // one launch: the FC heads inside the trunk kernel
-        if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
-            (filters != 64 && filters != 128))
-            return RVZ_EINVAL;
-        if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
-        if (n == 0) return RVZ_OK;
-        hipStream_t s = (hipStream_t)stream;
-        if (board == 8)
-            launch_trunk_h2<8>(x, n, params, blob, filters, blocks, work, logits, value, s, n_live);
-        else
-            launch_trunk_h2<6>(x, n, params, blob, filters, blocks, work, logits, value, s, n_live);
-        return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
-    }
     const int rc = rvz_resnet_trunk_h2_ex(board, x, n, params, blob, filters, blocks, work, n_live,
                                           nullptr, nullptr, 0, stream);
     if (rc != RVZ_OK) return rc;

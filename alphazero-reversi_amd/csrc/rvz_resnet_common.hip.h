@@ -1,0 +1,266 @@
+// rvz_resnet_common.hip.h — pieces of the policy/value ResNet kernels shared by the product
+// evaluator (csrc/rvz_resnet.hip, k_resnet_h2 + k_heads_mfma) and the A/B / cross-check build
+// (tools/alt/rvz_resnet_alt.hip): the packed parameter layout, the 1x1 head convs, the batched FC
+// heads on the f32 matrix cores, the compacted-batch row test and the phase-timing stamps.
+// Packed parameter buffer (fp32, BN folded by rvz.network.pack_resnet_params; every segment starts
+// 16-byte aligned; offsets in make_layout):
+//   stem_w[F][27] (k = tap*3 + ch), stem_b[F], res_w[2NB][9][F(n)][F(k)], res_b[2NB][F],
+//   pol_w[2][F], pol_b[2], pfc_w[65][128] (in = c*64 + px), pfc_b[65], val_w[F], val_b[1],
+//   vfc1_w[256][64], vfc1_b[256], vfc2_w[256], vfc2_b[1].
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/rvz.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+struct Layout {
+    int64_t stem_w, stem_b, res_w, res_b, pol_w, pol_b, pfc_w, pfc_b, val_w, val_b, vfc1_w,
+        vfc1_b, vfc2_w, vfc2_b, total;
+};
+
+__host__ __device__ inline int64_t al4(int64_t o) { return (o + 3) & ~int64_t(3); }
+
+__host__ __device__ inline Layout make_layout(int F, int NB, int BS = 8) {
+    Layout L;
+    const int cells = BS * BS;
+    int64_t o = 0;
+    L.stem_w = o; o = al4(o + (int64_t)F * 27);
+    L.stem_b = o; o = al4(o + F);
+    L.res_w = o;  o = al4(o + (int64_t)2 * NB * 9 * F * F);
+    L.res_b = o;  o = al4(o + (int64_t)2 * NB * F);
+    L.pol_w = o;  o = al4(o + 2 * F);
+    L.pol_b = o;  o = al4(o + 2);
+    L.pfc_w = o;  o = al4(o + (int64_t)(cells + 1) * 2 * cells);
+    L.pfc_b = o;  o = al4(o + cells + 1);
+    L.val_w = o;  o = al4(o + F);
+    L.val_b = o;  o = al4(o + 1);
+    L.vfc1_w = o; o = al4(o + 256 * cells);
+    L.vfc1_b = o; o = al4(o + 256);
+    L.vfc2_w = o; o = al4(o + 256);
+    L.vfc2_b = o; o = al4(o + 1);
+    L.total = o;
+    return L;
+}
+
+// heads (network.py:104-117), part 1: the 1x1 convs (BN folded) + ReLU of both heads, in one
+// pass over the activations: lane = pixel, wave = (board, channel group), partial sums per group
+// through LDS (`part`, the free ping-pong buffer) added in a fixed order. Writes, per board b
+// (cells = BS*BS), hpv(b)[0 .. 2 cells) = the policy planes (NCHW flatten, the FC's input order)
+// and hpv(b)[2 cells .. 3 cells) = the value plane. A BS < 8 board sits in the top-left corner
+// of the 8x8 pixel grid.
+template <int F, int NBOARD, int NTHR, int BS = 8, bool PACKED = false, bool ILV = false, class Act,
+          class Out>
+__device__ __forceinline__ void head_convs(const Act& act, float* part,
+                                           const float* __restrict__ prm, const Layout& L,
+                                           const Out& hpv, int tid) {
+    constexpr int NW = NTHR / 64, CG = NW / NBOARD, CPG = F / CG;
+    static_assert(CPG % 8 == 0, "8-channel reads");
+    const int lane = tid & 63;
+    {
+        const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+        // PACKED: board b's cells are act rows b * BS^2 + cell (h2); else the 8x8 grid
+        const int b = wave % NBOARD, cg = wave / NBOARD, row = b * 64 + lane;
+        // ILV (k_resnet_h2, two 8x8 boards): cell (r, c) of board b is act row r * 16 + b * 8 + c
+        const int arow = ILV ? (lane >> 3) * 16 + b * 8 + (lane & 7)
+                             : (PACKED ? b * BS * BS + lane : row);
+        const bool on = !PACKED || lane < BS * BS;
+        const float* w0 = prm + L.pol_w + cg * CPG;
+        const float* w1 = w0 + F;
+        const float* w2 = prm + L.val_w + cg * CPG;
+        float p0 = 0.0f, p1 = 0.0f, p2 = 0.0f;
+#pragma unroll
+        for (int k8 = 0; k8 < CPG / 8; ++k8) {
+            if (!on) break;
+            float v[8];
+            act.load8(arow, cg * CPG + 8 * k8, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                p0 = fmaf(v[j], w0[8 * k8 + j], p0);
+                p1 = fmaf(v[j], w1[8 * k8 + j], p1);
+                p2 = fmaf(v[j], w2[8 * k8 + j], p2);
+            }
+        }
+        part[(cg * 3 + 0) * NBOARD * 64 + row] = p0;
+        part[(cg * 3 + 1) * NBOARD * 64 + row] = p1;
+        part[(cg * 3 + 2) * NBOARD * 64 + row] = p2;
+    }
+    __syncthreads();
+    constexpr int CELLS = BS * BS;
+    for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
+        const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
+        const int b = rem / CELLS, cell = rem % CELLS;
+        const int row = b * 64 + (PACKED ? cell : (cell / BS) * 8 + cell % BS);
+        float acc = 0.0f;
+#pragma unroll
+        for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * NBOARD * 64 + row];
+        const float bias = c2 < 2 ? prm[L.pol_b + c2] : prm[L.val_b];
+        hpv.store(b, c2 * CELLS + cell, fmaxf(acc + bias, 0.0f));
+    }
+}
+struct HeadsLds {        // hpv rows in LDS
+    float* p;
+    __device__ void store(int b, int i, float v) const { p[b * 192 + i] = v; }
+};
+struct HeadsGlobal {     // hpv rows in the global workspace of rvz_resnet_fwd_split
+    float* p;
+    int g0, n_boards;
+    __device__ void store(int b, int i, float v) const {
+        if (g0 + b < n_boards) p[(size_t)(g0 + b) * 192 + i] = v;
+    }
+};
+
+// a compacted leaf batch (include/rvz.h RVZ_LIVE_STRIPE): is the row past its stripe's live count?
+__device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int row) {
+    return n_live && row % RVZ_LIVE_STRIPE >= n_live[row / RVZ_LIVE_STRIPE * RVZ_LIVE_PITCH];
+}
+
+// heads, part 2 on the f32 matrix cores (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32
+// accumulation — the arithmetic of an fp32 GEMM), 16 boards per workgroup: D = W X^T with rows =
+// output units (16-unit tiles: value fc1 16 tiles, policy fc ceil((cells+1)/16)), columns = the
+// 16 boards. The K order is permuted (step 4j + i uses k = 16j + 4g + i for lane group
+// g = lane >> 4), so a lane loads 4 consecutive k of its weight row (f32x4, L2) and of its
+// board's input row (ds_read_b128) per 4 MFMAs. Value fc2 (256 -> 1) + tanh reduce the fc1 tiles
+// through registers, lane shuffles and 64 floats of LDS.
+template <int BS>
+__global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ work, int n,
+                                                    const float* __restrict__ prm, Layout L,
+                                                    float* __restrict__ logits,
+                                                    float* __restrict__ value,
+                                                    const int32_t* __restrict__ n_live,
+                                                    uint32_t* __restrict__ stamp_ctr) {
+    // bench.py: the trunk launch before this one is complete; advance its stamp ring
+    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
+    if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
+    constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
+    constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
+    constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
+    constexpr int VJ = VK / 16, PJ = PK / 16, VTW = 256 / 16 / 4, PTW = (PT + 3) / 4;
+    static_assert(CELLS % 4 == 0 && PIN % 4 == 0, "f32x4 rows");
+    __shared__ __attribute__((aligned(16))) float in[16 * ROW];
+    __shared__ float vpart[4][16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g0 = blockIdx.x * 16, col = lane & 15, grp = lane >> 4;
+    // every weight fragment of this wave's tiles, issued before anything waits: value fc1 tiles
+    // wave + 4m, policy tiles wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
+    f32x4 av[VTW][VJ], ap[PTW][PJ];
+#pragma unroll
+    for (int m = 0; m < VTW; ++m) {
+        const float* wr = prm + L.vfc1_w + (size_t)(16 * (wave + 4 * m) + col) * CELLS + 4 * grp;
+#pragma unroll
+        for (int j = 0; j < VJ; ++j)
+            av[m][j] = 16 * j + 4 * grp < CELLS ? *reinterpret_cast<const f32x4*>(wr + 16 * j)
+                                                : f32x4{};
+    }
+#pragma unroll
+    for (int m = 0; m < PTW; ++m) {
+        const int o = 16 * (wave + 4 * m) + col;
+        const float* wr = prm + L.pfc_w + (size_t)o * PIN + 4 * grp;
+#pragma unroll
+        for (int j = 0; j < PJ; ++j)
+            ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
+                           ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
+    }
+    for (int i = tid; i < 16 * (PK + VK); i += 256) {
+        const int b = i / (PK + VK), k = i % (PK + VK), g = g0 + b;
+        float v = 0.0f;
+        if (g < n) {
+            if (k < PIN) v = work[(size_t)g * 192 + k];
+            else if (k >= PK && k - PK < CELLS) v = work[(size_t)g * 192 + PIN + (k - PK)];
+        }
+        in[b * ROW + k] = v;
+    }
+    __syncthreads();
+    const float* inb = in + col * ROW + 4 * grp;
+    // value fc1 (+ bias, ReLU) and its fc2 partial
+    float vp = 0.0f;
+#pragma unroll
+    for (int m = 0; m < VTW; ++m) {
+        f32x4 acc = {};
+#pragma unroll
+        for (int j = 0; j < VJ; ++j) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + PK + 16 * j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][j][i], bx[i], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {                // D row = unit 16t + 4grp + r, col = board
+            const int uu = 16 * (wave + 4 * m) + 4 * grp + r;
+            vp = fmaf(fmaxf(acc[r] + prm[L.vfc1_b + uu], 0.0f), prm[L.vfc2_w + uu], vp);
+        }
+    }
+    vp += __shfl_xor(vp, 16);
+    vp += __shfl_xor(vp, 32);
+    if (grp == 0) vpart[wave][col] = vp;
+    // policy fc
+#pragma unroll
+    for (int m = 0; m < PTW; ++m) {
+        const int t = wave + 4 * m;
+        if (t >= PT) break;
+        f32x4 acc = {};
+#pragma unroll
+        for (int j = 0; j < PJ; ++j) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + 16 * j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[m][j][i], bx[i], acc, 0, 0, 0);
+        }
+        const int g = g0 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int oo = 16 * t + 4 * grp + r;
+            if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
+        }
+    }
+    __syncthreads();
+    if (tid < 16 && g0 + tid < n)
+        value[g0 + tid] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
+                                prm[L.vfc2_b]);
+}
+
+#ifdef RVZ_PHASE_TIMING   // tools/phase_timing.py: per-workgroup s_memtime at phase boundaries
+__device__ uint64_t g_phase[65536][8];
+__device__ uint64_t g_rt[65536][2];   // s_memrealtime (100 MHz) at start / end
+__device__ uint64_t g_wave[65536][16];
+#define PHASE(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_phase[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
+#define RT(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_rt[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime()
+__device__ uint64_t g_stem[65536][8];
+__device__ uint32_t g_hwid[65536][2];   // HW_ID (CU, SE, ...), XCC_ID of each workgroup
+#define HWID() \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) { \
+        g_hwid[blockIdx.x][0] = __builtin_amdgcn_s_getreg((31 << 11) | 4); \
+        g_hwid[blockIdx.x][1] = __builtin_amdgcn_s_getreg((31 << 11) | 20); \
+    }
+#define STEM_T(i) \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_stem[blockIdx.x][i] = __builtin_amdgcn_s_memtime()
+#define WAVE_T(i) \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 65536) \
+        g_wave[blockIdx.x][(threadIdx.x >> 6) + 8 * (i)] = __builtin_amdgcn_s_memtime()
+#else
+#define PHASE(i)
+#define HWID()
+#define STEM_T(i)
+#define WAVE_T(i)
+#define RT(i)
+#endif
+
+// sched_group_barrier pattern: NM MFMAs, the first ND gaps get one LDS read, the next NV one
+// global load
+template <int I, int NM, int ND, int NV>
+__device__ __forceinline__ void interleave_loads() {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if constexpr (I < ND) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    else if constexpr (I < ND + NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    if constexpr (I + 1 < NM) interleave_loads<I + 1, NM, ND, NV>();
+}
+
+}  // namespace

@@ -78,16 +78,8 @@ SIGNATURES = {
     "rvz_tree_nodes": (C.c_int, [_P]),
     "rvz_tree_export": (C.c_int, [_P, _P, _P]),
     "rvz_footprint": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
-    "rvz_nn_bias_act_f32": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
-    "rvz_nn_bias_act_bf16": (C.c_int, [_P, _P, _P, C.c_int64, C.c_int32, C.c_int32, _P]),
     "rvz_resnet_params_size": (C.c_int64, [C.c_int32, C.c_int32, C.c_int32]),
-    "rvz_resnet_fwd_f32": (C.c_int, [C.c_int32, _P, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P,
-                                     _P]),
-    "rvz_resnet_split_size": (C.c_int64, [C.c_int32, C.c_int32]),
-    "rvz_resnet_split_weights": (C.c_int, [_P, C.c_int32, C.c_int32, _P, _P]),
     "rvz_resnet_work_size": (C.c_int64, [C.c_int32]),
-    "rvz_resnet_trunk_split": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32,
-                                         _P, _P]),
     "rvz_resnet_heads_fc": (C.c_int, [C.c_int32, _P, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P,
                                       _P]),
     "rvz_resnet_h2_size": (C.c_int64, [C.c_int32, C.c_int32]),
@@ -96,8 +88,6 @@ SIGNATURES = {
                                       _P, _P]),
     "rvz_resnet_fwd_h2": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32, _P,
                                     _P, _P, _P]),
-    "rvz_resnet_fwd_split": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32, _P,
-                                       _P, _P, _P]),
 }
 
 _lib = None

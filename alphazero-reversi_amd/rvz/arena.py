@@ -4,8 +4,10 @@
 leaderboard, JSON save/load). ``ELOPlayer`` and ``Arena`` keep the reference's API
 (``add_player``, ``play_game``, ``run_tournament``, ``print_leaderboard``, ``save_results``), but
 the games of a matchup are played in lockstep on the GPU: one rvz engine per player (its own MCTS
-parameters and evaluator) searches every game each ply, and the move of the player to move is
-applied — the reference's ``current_player.get_move(game)`` (arena.py:244-262) for a whole batch.
+parameters and evaluator) searches, each ply, exactly the games in which that player is to move
+(the others are handed to its engine as finished, so they cost no search and, with compacted leaf
+batches, no NN rows), and applies its moves — the reference's ``current_player.get_move(game)``
+(arena.py:244-262) for a whole batch.
 Results are then folded into the ratings in exactly the reference's game order, so the ELO
 history is what the sequential tournament would record for the same game outcomes.
 
@@ -93,7 +95,10 @@ class ELOPlayer:
     """A model player (MCTS with its own parameters) or, with model None, a random player."""
 
     def __init__(self, player_id: str, model=None, mcts_params: Optional[Dict] = None,
-                 device: str = "cuda", nn_dtype=torch.float32):
+                 device: str = "cuda", nn_dtype=torch.float32, evaluator=None):
+        """evaluator: the leaf evaluator of a model player (default LeafEvaluator(model), the h2
+        kernels); any callable leaf_x -> (logits, value) works (``outputs_probs = True``:
+        softmaxed rows)."""
         self.player_id = player_id
         self.model = model
         self.device = torch.device(device)
@@ -102,10 +107,12 @@ class ELOPlayer:
         self.c_puct = float(params.get("c_puct", 1.0))
         self.batch_size = int(params.get("batch_size", 64))
         self.evaluator = None
+        self.board_size = int(getattr(model, "board_size", 8))
         if model is not None:
             model.eval()
             model.to(self.device)
-            self.evaluator = LeafEvaluator(model, dtype=nn_dtype, device=self.device)
+            self.evaluator = evaluator if evaluator is not None else LeafEvaluator(
+                model, dtype=nn_dtype, device=self.device)
 
     def reset(self):
         """Searches start from a fresh root every move (mcts.py:334): nothing to reset."""
@@ -135,16 +142,22 @@ class Arena:
             if pid not in self.players:
                 raise ValueError(f"One or both players not found: {pid}")
         dev = next(iter(self.players[p].device for p in ids))
+        sizes = {self.players[p].board_size for p in ids if self.players[p].model is not None}
+        if len(sizes) > 1:
+            raise ValueError(f"players of one batch play on one board size, got {sorted(sizes)}")
+        bs = sizes.pop() if sizes else 8
+        nsq = bs * bs
         engines = {}
         for pid in ids:
             pl = self.players[pid]
             if pl.model is not None:
-                engines[pid] = Engine(G, pl.num_simulations, pl.batch_size, pl.c_puct, device=dev)
-        env = Engine(G, 64, 64, device=dev)          # the authoritative boards (env only)
+                engines[pid] = Engine(G, pl.num_simulations, pl.batch_size, pl.c_puct,
+                                      board_size=bs, device=dev, compact_leaves=True)
+        env = Engine(G, 64, 64, board_size=bs, device=dev)   # the authoritative boards (env only)
         env.reset(range(G))
         black = np.asarray([ids.index(b) for b in black_ids])
         white = np.asarray([ids.index(w) for w in white_ids])
-        for _ in range(60):                            # every move places a disc
+        for _ in range(nsq - 4):                       # every move places a disc
             b, w, st = env.get_state()
             status = st.cpu().numpy()
             if status[:, 1].all():
@@ -161,19 +174,27 @@ class Arena:
                 if pl.model is None:                   # random player: random.choice(valid)
                     legal = env.legal().cpu().numpy().view(np.uint64)
                     for g in np.flatnonzero(games_k):
-                        sq = [s for s in range(64) if (int(legal[g]) >> s) & 1]
+                        sq = [s for s in range(nsq) if (int(legal[g]) >> s) & 1]
                         move[g] = self.py_rng.choice(sq) if sq else -1
                     continue
                 eng = engines[pid]
-                eng.set_state(b, w, st)
+                # this player's games only: the others enter its engine as finished (no search)
+                st_k = st.clone()
+                st_k[:, 1] = torch.where(torch.from_numpy(games_k).to(dev), st[:, 1],
+                                         torch.ones_like(st[:, 1]))
+                eng.set_state(b, w, st_k)
                 eng.search(pl.evaluator)
                 idx, _ = eng.act(1.0, u=u, apply=False)   # arena.py:183-186 uses T = 1.0
                 idx = idx.cpu().numpy()
-                move[games_k] = np.where(idx[games_k] == 64, -1, idx[games_k])
+                move[games_k] = np.where(idx[games_k] == nsq, -1, idx[games_k])
             over = status[:, 1] != 0
-            sq = torch.from_numpy(np.where(over, 64, move).astype(np.int32)).to(dev)
+            sq = torch.from_numpy(np.where(over, nsq, move).astype(np.int32)).to(dev)
             env.apply(sq)                              # make_move; finished games reject it
+        for eng in engines.values():
+            eng.check()                                # device error words / evaluator overflow
         b, w, st = env.get_state()
+        if not bool(st[:, 1].all()):
+            raise RuntimeError("Arena.play_games: a game is not over after its last ply")
         bb = b.cpu().numpy().view(np.uint64)
         ww = w.cpu().numpy().view(np.uint64)
         res = []

@@ -36,8 +36,11 @@ HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense peaks, same source
 
 
-PRESETS = {   # BASELINE.json configs (index 0 is the reference's own single CPU game)
+PRESETS = {   # BASELINE.json configs
     # lanes: independent game lanes per GPU in one graph (same games; measured best per config)
+    # c1: the reference's own plumbing case (one game, 100 sims, the ModelConfig default 5x128
+    # net; config.py:14-15) on one GPU, with the CPU port on the same single game beside it
+    "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1),
     "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2),
     "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),
     # per GPU, x8; a step = one self-play + training iteration (main_c4)
@@ -245,7 +248,7 @@ def cpu_baseline(args, net):
     torch.set_num_threads(cores)
     cpu_net = make_net(args, "cpu")
     cpu_net.load_state_dict({k: v.cpu() for k, v in net.state_dict().items()})
-    G = 384                                   # ~10 s of C2 work on the GPU box's 16 host threads
+    G = min(384, args.games)                  # ~10 s of C2 work on the GPU box's 16 host threads
     games = [O.new_game(args.board) for _ in range(G)]
     mts = [O.MT(args.seed + g) for g in range(G)]
     srch = O.Search(G, args.sims, args.batch, 1.0, bs=args.board)
@@ -298,7 +301,8 @@ def cpu_baseline(args, net):
     return {"value": steps / dt, "unit": "board-steps/s", "cores": cores, "kind": "port",
             "sample": f"{G} games from the start position, {steps} plies in {dt:.1f}s, "
                       f"{args.sims} sims, oracle/ C search + {args.blocks}x{args.filters} net "
-                      f"fp32 on {cores} host threads",
+                      f"fp32 on {cores} host threads; one NN row per game per batch (the "
+                      f"reference evaluates {args.batch} identical rows, mcts.py:582-594)",
             "env_tree_only": {"value": G / dt_stub, "unit": "board-steps/s", "cores": cores,
                               "sample": f"{G} first-ply searches, zero-cost evaluator"},
             "env_tree_only_1core": one}
@@ -460,7 +464,13 @@ def main():
     leaf_dtype = torch.float32 if nn_dtype == torch.float32 else torch.bfloat16
 
     def make_ev():
-        return rvz.LeafEvaluator(net, dtype=nn_dtype, device=device, kernel=args.nn_kernel)
+        if args.nn_kernel in ("auto", "h2") and nn_dtype == torch.float32:
+            return rvz.LeafEvaluator(net, dtype=nn_dtype, device=device)
+        # A/B alternatives (not the product path): tools/alt/librvz_alt.so
+        sys.path.insert(0, os.path.join(ROOT, "tools", "alt"))
+        from alt_eval import AltEvaluator
+        return AltEvaluator(net, kernel="miopen" if args.nn_kernel in ("auto", "h2")
+                            else args.nn_kernel, dtype=nn_dtype, device=device)
 
     def make_eng(n):
         return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
@@ -602,7 +612,7 @@ def main():
                    "mfma_flops_per_row": fpr,
                    "fp32_equiv_tflops_isolated": round(nn_flops / (t_iso * 1e-3) / 1e12, 2)}
     else:
-        nn_roof = {"kernel": "rvz_resnet_fwd_f32" if ev.use_resnet else "miopen",
+        nn_roof = {"kernel": "rvz_resnet_fwd_f32" if ev.kernel == "resnet" else "miopen",
                    "bound": "mfma", "achieved": round(nn_tflops, 2),
                    "peak": MFMA_PEAK_TFLOPS[args.nn_dtype], "unit": "TFLOP/s",
                    "frac": round(nn_tflops / MFMA_PEAK_TFLOPS[args.nn_dtype], 4), "traffic": None}

@@ -173,53 +173,24 @@ int rvz_tree_export(rvz_engine *e, void *nodes_out, uint32_t *meta_out);
 /* Sizes of the engine's device-resident state, for DESIGN/bench accounting (host out). */
 int rvz_footprint(const rvz_engine *e, int64_t *bytes_tree, int64_t *bytes_env);
 
-/* ---- leaf-evaluator helpers (the policy/value net, not the reference path) -- */
-/* In place over an NHWC (channels_last) activation of n_pix pixels x channels (conv output with
- * the BN-folded conv bias not yet added): x = act(x + bias[c] (+ residual)), act = ReLU when
- * relu != 0 — network.py:23-28,97's bias/BN, skip add and ReLU in one pass. residual may be NULL.
- * f32: channels % 4 == 0; bf16 (x, residual bf16, bias f32): channels % 8 == 0. */
-int rvz_nn_bias_act_f32(float *x, const float *bias, const float *residual, int64_t n_pix,
-                        int32_t channels, int32_t relu, void *hip_stream);
-int rvz_nn_bias_act_bf16(void *x, const float *bias, const void *residual, int64_t n_pix,
-                         int32_t channels, int32_t relu, void *hip_stream);
-
-/* The whole policy/value network forward (network.py:30-117, BN folded) in one kernel: x float32
+/* ---- the leaf evaluator (the policy/value net, the boundary's callee) ---- */
+/* The reference's AlphaZeroNetwork forward (network.py:30-117, BN folded): x float32
  * [n, 3, board, board] (the leaf planes) -> logits float32 [n, board^2 + 1], value float32 [n].
- * params: the packed fp32 buffer laid out as in csrc/rvz_resnet.hip
+ * params: the packed fp32 buffer laid out as in csrc/rvz_resnet_common.hip.h
  * (rvz.network.pack_resnet_params), 16-byte aligned, of rvz_resnet_params_size(board, filters,
  * blocks) floats (negative: unsupported shape). filters 64 or 128, any block count.
- * rvz_resnet_fwd_f32: board 8 only; fp32 on the f32-input MFMA, activations resident in LDS. */
+ * work: float scratch of rvz_resnet_work_size(n) elements (the 1x1-conv head outputs handed from
+ * the trunk launch to the FC-heads launch, + the overflow word). */
 int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks);
-int rvz_resnet_fwd_f32(int32_t board, const float *x, int32_t n, const float *params,
-                       int32_t filters, int32_t blocks, float *logits, float *value,
-                       void *hip_stream);
-
-/* The same forward with fp32 arithmetic emulated on the bf16 MFMA: every operand split exactly
- * into three bf16 parts (x = x0 + (x1 + x2)) and the six partial products of weight >= 2^-16
- * accumulated in fp32 (error of an fp32 GEMM; see csrc/rvz_resnet.hip). Boards 8 and 6.
- * wsplit: the conv weights re-laid out by rvz_resnet_split_weights from the packed params (once
- * per parameter update), rvz_resnet_split_size(filters, blocks) uint16 elements, 16-byte
- * aligned. work: float scratch of rvz_resnet_work_size(n) elements (the 1x1-conv head outputs
- * handed to the FC launch). */
-int64_t rvz_resnet_split_size(int32_t filters, int32_t blocks);
-int rvz_resnet_split_weights(const float *params, int32_t filters, int32_t blocks,
-                             uint16_t *wsplit, void *hip_stream);
 int64_t rvz_resnet_work_size(int32_t n);
-int rvz_resnet_fwd_split(int32_t board, const float *x, int32_t n, const float *params,
-                         const uint16_t *wsplit, int32_t filters, int32_t blocks, float *work,
-                         float *logits, float *value, void *hip_stream);
-/* rvz_resnet_fwd_split's two launches on their own: the trunk (stem, residual tower, 1x1 head
- * convs -> work) and the batched FC heads (work -> logits, value). */
-int rvz_resnet_trunk_split(int32_t board, const float *x, int32_t n, const float *params,
-                           const uint16_t *wsplit, int32_t filters, int32_t blocks, float *work,
-                           void *hip_stream);
+/* The batched FC heads alone (work -> logits, value; f32 MFMA, fp32 products and sums). */
 int rvz_resnet_heads_fc(int32_t board, const float *work, int32_t n, const float *params,
                         int32_t filters, int32_t blocks, float *logits, float *value,
                         void *hip_stream);
 
-/* The same forward, fp32 emulated on the f16 MFMA with two parts per operand (the default leaf
- * evaluator): x = x0 + x1 (f16 each, 22 significant bits), weights pre-scaled per output channel
- * by a power of two, the three partial products x0w0 + x0w1 + x1w0 accumulated in one fp32
+/* The forward, fp32 emulated on the f16 MFMA with two parts per operand (the leaf evaluator):
+ * x = x0 + x1 (f16 each, 22 significant bits), weights pre-scaled per output channel by a power
+ * of two, the three partial products x0w0 + x0w1 + x1w0 accumulated in one fp32
  * accumulator (error of an fp32 GEMM; see csrc/rvz_resnet.hip k_resnet_h2). Boards 8 and 6.
  * blob: rvz_resnet_h2_weights' output (scaled f16 parts + inverse scales, once per parameter
  * update), rvz_resnet_h2_size(filters, blocks) uint16 elements, 16-byte aligned.

@@ -4,7 +4,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (ROOT, os.path.join(ROOT, "alphazero-reversi_amd"), os.path.dirname(os.path.abspath(__file__))):
+for p in (ROOT, os.path.join(ROOT, "alphazero-reversi_amd"), os.path.join(ROOT, "tools", "alt"),
+          os.path.dirname(os.path.abspath(__file__))):
     if p not in sys.path:
         sys.path.insert(0, p)
 

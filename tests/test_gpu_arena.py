@@ -10,9 +10,9 @@ def _players():
     import rvz
     from rvz.arena import ELOPlayer
     torch.manual_seed(0)
-    a = rvz.AlphaZeroNetwork(8, 1, 16)
+    a = rvz.AlphaZeroNetwork(8, 1, 64)
     torch.manual_seed(1)
-    b = rvz.AlphaZeroNetwork(8, 1, 16)
+    b = rvz.AlphaZeroNetwork(8, 1, 64)
     params = {"num_simulations": 128, "c_puct": 1.0}
     return [ELOPlayer("net_a", a, params), ELOPlayer("net_b", b, {"num_simulations": 192}),
             ELOPlayer("random", None)]
@@ -42,3 +42,102 @@ def test_play_games_results_and_colours():
     r1 = arena.play_games(["net_a"] * 8 + ["random"] * 8, ["random"] * 8 + ["net_a"] * 8)
     assert len(r1) == 16 and set(r1) <= {0.0, 0.5, 1.0}
     assert arena.play_game("net_b", "net_a") in (0.0, 0.5, 1.0)
+
+
+class _TableEvaluator:
+    """A deterministic leaf evaluator with exact fp32 arithmetic on both sides (GPU torch here,
+    NumPy in the restatement): priors ((5 i + own discs) mod 8 + 1) / 16, pass 1/32, value
+    (own - opponent discs) / 64 — dyadic rationals, so the GPU and CPU searches see identical
+    NN outputs and any difference is the arena's."""
+    outputs_probs = True
+
+    def __call__(self, x):
+        own = x[:, 0].reshape(x.shape[0], -1).sum(1)
+        opp = x[:, 1].reshape(x.shape[0], -1).sum(1)
+        i = torch.arange(64, device=x.device, dtype=torch.float32)
+        p = torch.empty(x.shape[0], 65, device=x.device)
+        p[:, :64] = (torch.remainder(5 * i[None, :] + own[:, None], 8) + 1) / 16
+        p[:, 64] = 1 / 32
+        return p.contiguous(), ((own - opp) / 64).float().contiguous()
+
+    @staticmethod
+    def numpy(x):
+        own = x[:, 0].reshape(len(x), -1).sum(1).astype(np.float32)
+        opp = x[:, 1].reshape(len(x), -1).sum(1).astype(np.float32)
+        i = np.arange(64, dtype=np.float32)
+        p = np.empty((len(x), 65), np.float32)
+        p[:, :64] = (np.remainder(5 * i[None, :] + own[:, None], 8) + 1) / 16
+        p[:, 64] = 1 / 32
+        return p, ((own - opp) / 64).astype(np.float32)
+
+
+def _literal_arena(O, players, black_ids, white_ids, seed):
+    """The reference's game loop (arena.py:218-286: while not over, the player to move's
+    get_move, make_move; winner by disc count; ELOPlayer.get_move arena.py:175-188: MCTS
+    get_action_probs at T = 1, random.choice for a random player) on the CPU oracle, game by game
+    within each lockstep ply, with the batched arena's documented draw order: one
+    random_sample() per game per ply from RandomState(seed), random.Random(seed) choices in
+    (sorted player id, game) order."""
+    import random
+    np_rng, py_rng = np.random.RandomState(seed), random.Random(seed)
+    G = len(black_ids)
+    ids = sorted(set(black_ids) | set(white_ids))
+    games = [O.new_game() for _ in range(G)]
+    for _ in range(60):
+        if all(g.over for g in games):
+            break
+        u = np_rng.random_sample(G)
+        move = [-1] * G
+        for pid in ids:
+            mine = [g for g in range(G) if not games[g].over and
+                    (black_ids[g] if games[g].side == 1 else white_ids[g]) == pid]
+            if not mine:
+                continue
+            sims = players[pid]
+            if sims is None:
+                for g in mine:
+                    P, Q = (games[g].black, games[g].white) if games[g].side == 1 else \
+                        (games[g].white, games[g].black)
+                    lg = O.legal(P, Q)
+                    sq = [s for s in range(64) if (lg >> s) & 1]
+                    move[g] = py_rng.choice(sq) if sq else -1
+                continue
+            srch = O.Search(len(mine), sims, 64, 1.0)
+            srch.begin([games[g] for g in mine])
+            while (r := srch.step()) is not None:
+                p, v = _TableEvaluator.numpy(O.leaf_planes(r[0]))
+                srch.submit(p, v)
+            vis = srch.visits()
+            for j, g in enumerate(mine):
+                idx, _, _ = O.action(vis[j], 1.0, float(u[g]))
+                move[g] = -1 if idx == 64 else idx
+        for g in range(G):
+            if not games[g].over:
+                assert O.make_move(games[g], move[g])
+    res = []
+    for g in games:
+        nb, nw = bin(g.black).count("1"), bin(g.white).count("1")
+        res.append(1.0 if nb > nw else (0.0 if nw > nb else 0.5))
+    return res
+
+
+def test_play_games_matches_literal_reference_loop(oracle):
+    """Arena.play_games (lockstep, one engine per player searching only its own games) == the
+    reference's per-game loop restated on the CPU oracle with the same evaluator and draws:
+    every game's result. Players: two MCTS players (128 and 192 simulations) and a random
+    player, in every pairing and both colours. (At S <= 64 = one batch the root's children are
+    never visited, get_action_probs falls back to argmax(0s) = square 0, which is illegal: the
+    reference's arena loop then never ends; rvz raises instead.)"""
+    import rvz
+    from rvz.arena import Arena, ELOPlayer
+    net = rvz.AlphaZeroNetwork(8, 1, 64)
+    arena = Arena(seed=11)
+    arena.add_player(ELOPlayer("a", net, {"num_simulations": 128}, evaluator=_TableEvaluator()))
+    arena.add_player(ELOPlayer("b", net, {"num_simulations": 192}, evaluator=_TableEvaluator()))
+    arena.add_player(ELOPlayer("r", None))
+    pairs = [("a", "b"), ("b", "a"), ("a", "r"), ("r", "a"), ("b", "r"), ("r", "b"), ("a", "a")]
+    black = [p[0] for p in pairs for _ in range(3)]
+    white = [p[1] for p in pairs for _ in range(3)]
+    got = arena.play_games(black, white)
+    want = _literal_arena(oracle, {"a": 128, "b": 192, "r": None}, black, white, seed=11)
+    assert got == want

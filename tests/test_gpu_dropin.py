@@ -67,7 +67,7 @@ def test_mcts_dropin_matches_oracle(oracle):
 def test_selfplay_dropin_records(tmp_path):
     import rvz
     torch.manual_seed(0)
-    net = rvz.AlphaZeroNetwork(8, 2, 32).cuda()
+    net = rvz.AlphaZeroNetwork(8, 2, 64).cuda()
     sp = rvz.SelfPlay(net, {"num_simulations": 128, "c_puct": 1.0, "temperature": 1.0,
                             "save_dir": str(tmp_path), "seed": 3})
     games = sp.generate_games(8)
@@ -120,7 +120,7 @@ def test_ddp_trainer_single_gpu_step_on_records():
     import rvz
     from rvz.trainer import DDPTrainer
     torch.manual_seed(0)
-    net = rvz.AlphaZeroNetwork(8, 2, 32).cuda()
+    net = rvz.AlphaZeroNetwork(8, 2, 64).cuda()
     sp = rvz.SelfPlay(net, {"num_simulations": 128, "save_dir": "/tmp/rvz_sp_test", "seed": 9})
     sp.generate_games(16)
     data = sp.training_tensors()
@@ -135,7 +135,7 @@ def test_selfplay_runner_graph_replay_equals_eager():
     """One ply captured in a HIP graph and replayed == the same plies run eagerly (bit-exact)."""
     import rvz
     torch.manual_seed(0)
-    net = rvz.AlphaZeroNetwork(8, 2, 32).cuda().eval()
+    net = rvz.AlphaZeroNetwork(8, 2, 64).cuda().eval()
     ev = rvz.LeafEvaluator(net)
     outs = []
     for graph in (False, True):

@@ -5,12 +5,15 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from evaluators import make_evaluator  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("relu", [False, True])
 def test_bias_act_f32_bit_exact(res, relu):
+    import alt_eval
     from rvz import _lib
     cl = torch.channels_last
     torch.manual_seed(1)
@@ -23,13 +26,14 @@ def test_bias_act_f32_bit_exact(res, relu):
     if relu:
         ref = F.relu(ref)
     y = x.clone(memory_format=cl)
-    _lib.check(_lib.load().rvz_nn_bias_act_f32(y.data_ptr(), b.data_ptr(),
+    _lib.check(alt_eval.load().rvz_nn_bias_act_f32(y.data_ptr(), b.data_ptr(),
                                               r.data_ptr() if res else None, 1000 * 64, 64,
                                               int(relu), _lib.stream_handle()), None, "bias_act")
     assert torch.equal(y, ref)
 
 
 def test_bias_act_bf16_close():
+    import alt_eval
     from rvz import _lib
     cl = torch.channels_last
     x = torch.randn(512, 64, 8, 8, device="cuda").to(torch.bfloat16).contiguous(memory_format=cl)
@@ -37,7 +41,7 @@ def test_bias_act_bf16_close():
     b = torch.randn(64, device="cuda")
     ref = F.relu(x.float() + b.view(1, -1, 1, 1) + r.float()).to(torch.bfloat16)
     y = x.clone(memory_format=cl)
-    _lib.check(_lib.load().rvz_nn_bias_act_bf16(y.data_ptr(), b.data_ptr(), r.data_ptr(),
+    _lib.check(alt_eval.load().rvz_nn_bias_act_bf16(y.data_ptr(), b.data_ptr(), r.data_ptr(),
                                                512 * 64, 64, 1, _lib.stream_handle()), None, "b")
     assert (y.float() - ref.float()).abs().max().item() <= 2 ** -7 * ref.float().abs().max().item()
 
@@ -56,15 +60,16 @@ def test_evaluator_fp32_matches_module(blocks, filters):
     with torch.no_grad():
         lr, vr = net(x)
     scale = lr.abs().max().item()
-    for fused, kern in ((True, "miopen"), (False, "miopen"), (True, "auto")):
-        ev = rvz.LeafEvaluator(net, fused_epilogue=fused, kernel=kern)
+    kinds = ((True, "miopen"), (False, "miopen")) + (((True, "h2"),) if filters in (64, 128) else ())
+    for fused, kern in kinds:
+        ev = make_evaluator(net, kern, fused_epilogue=fused)
         l, v = ev(x)
         # fp32 throughout; only the summation order differs (BN folding, NHWC igemm vs NCHW)
         assert (l - lr).abs().max().item() <= 2e-5 * scale
         assert (v - vr).abs().max().item() <= 2e-3   # tanh of large random-init activations
         pr = torch.softmax(lr, 1)
         assert (torch.softmax(l, 1) - pr).abs().max().item() <= 1e-4
-    evb = rvz.LeafEvaluator(net, dtype=torch.bfloat16)     # throughput mode, not parity grade
+    evb = make_evaluator(net, "miopen", dtype=torch.bfloat16)     # throughput mode, not parity grade
     lb, vb = evb(x)
     # bf16 activations: ~3 significant digits on logits of a deep random-init net
     assert (lb - lr).abs().max().item() <= 0.05 * scale
@@ -103,7 +108,7 @@ def test_split_kernel_6x6_matches_module(blocks, filters, n):
         lr, vr = net(x)
     assert rvz.LeafEvaluator(net).kernel == "h2"
     for kern in ("h2", "split"):
-        l, v = rvz.LeafEvaluator(net, kernel=kern)(x)
+        l, v = make_evaluator(net, kern)(x)
         torch.cuda.synchronize()
         assert l.shape == (n, 37)
         scale = lr.abs().max().item()
@@ -122,8 +127,8 @@ def test_resnet_kernel_matches_module(kernel, blocks, filters, n):
     x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
     with torch.no_grad():
         lr, vr = net(x)
-    ev = rvz.LeafEvaluator(net, kernel=kernel)
-    assert ev.use_resnet and ev.kernel == kernel
+    ev = make_evaluator(net, kernel)
+    assert ev.kernel == kernel
     l, v = ev(x)
     torch.cuda.synchronize()
     scale = lr.abs().max().item()
@@ -145,7 +150,7 @@ def test_split_error_is_fp32_class(blocks, filters, n):
         lm, vm = net(x)
     err = {}
     for kern in ("resnet", "split", "h2"):
-        l, v = rvz.LeafEvaluator(net, kernel=kern)(x)
+        l, v = make_evaluator(net, kern)(x)
         err[kern] = (l.double().cpu() - l64).abs().max().item()
     err["module"] = (lm.double().cpu() - l64).abs().max().item()
     scale = l64.abs().max().item()
@@ -170,7 +175,7 @@ def test_evaluator_matches_reference_outputs(kernel):
                                                   "mcts_s800_6x64.npz"))
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
-    ev = rvz.LeafEvaluator(net, kernel=kernel)
+    ev = make_evaluator(net, kernel)
     logits, v = ev(torch.from_numpy(x).cuda())
     p = torch.softmax(logits, 1).cpu().numpy()
     dp = np.abs(p - probs).max()
@@ -205,7 +210,9 @@ def test_h2_weight_blob():
     blob = ev.wsplit.cpu().numpy().view(np.uint16)
     F, NB, K, TM = 64, 1, 32, 16
     layer = 9 * F * F * 2
-    stem_off = 2 * NB * layer + 4 * 2 * F * K
+    pad_ksteps = 4                       # h2_pad_ksteps: the weight prefetch past the last layer
+    stem_off = 2 * NB * layer + pad_ksteps * 2 * F * K
+    assert not blob[2 * NB * layer:stem_off].any()
     sc_off = stem_off + 2 * F * K
     isc = blob[sc_off:sc_off + 2 * (1 + 2 * NB) * F].view(np.float32).reshape(1 + 2 * NB, F)
     assert np.all(np.log2(isc) == np.round(np.log2(isc)))

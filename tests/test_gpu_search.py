@@ -213,6 +213,47 @@ def test_full_size_invariants_32768():
     assert (vis.sum(1) == 736).all()
 
 
+def test_c3_workload_two_plies(oracle):
+    """C3 as configured (BASELINE.json configs[2]): 32,768 games x 800 sims with the 10x128 h2
+    evaluator, compacted leaf batches, two plies. Properties of every game (no device error, no
+    activation overflow, 736 = 800 - 64 root-child visits in the opening, every move legal) and,
+    for 16 sampled games, the visit counts and moves of the literal oracle search fed by the
+    same evaluator (an h2 row's outputs do not depend on its batch position)."""
+    import rvz
+    G, S = 32768, 800
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 10, 128).cuda().eval()
+    ev = rvz.LeafEvaluator(net)
+    eng = rvz.Engine(G, num_simulations=S, batch_size=64, compact_leaves=True)
+    eng.reset(range(G))
+    sample = np.linspace(0, G - 1, 16).astype(int)
+    games = [oracle.new_game() for _ in sample]
+    mts = [oracle.MT(int(g)) for g in sample]
+    for ply in range(2):
+        b0, w0, st0 = (t.clone() for t in eng.get_state())
+        eng.search(ev, fused_softmax=False)          # torch's F.softmax on both sides
+        vis = eng.visits().cpu().numpy().copy()
+        idx, _ = eng.act(1.0, apply=True)
+        idx = idx.cpu().numpy()
+        eng.check()
+        assert (vis.sum(1) == S - 64).all()
+        legal = rvz.board_legal(b0, w0, st0).cpu().numpy().view(np.uint64)
+        assert all((int(legal[g]) >> int(idx[g])) & 1 for g in range(G))
+        srch = oracle.Search(len(sample), S, 64, 1.0)
+        srch.begin(games)
+        while (r := srch.step()) is not None:
+            x = torch.from_numpy(oracle.leaf_planes(r[0])).cuda()
+            lo, vo = ev(x)
+            srch.submit(torch.softmax(lo, 1).cpu().numpy(), vo.cpu().numpy())
+        ov = srch.visits()
+        assert np.array_equal(ov, vis[sample]), ply
+        for j, g in enumerate(sample):
+            a, _, _ = oracle.action(ov[j], 1.0, mts[j].random_sample())
+            assert a == idx[g]
+            assert oracle.make_move(games[j], a)
+    assert not ev.overflowed()
+
+
 def test_bf16_leaf_planes_equal_f32():
     import rvz
     G = 512

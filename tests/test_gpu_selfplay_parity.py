@@ -16,6 +16,8 @@ import torch
 
 import golden_replay as R
 
+from evaluators import make_evaluator  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -81,8 +83,8 @@ def test_accepts_live_count_is_a_real_property():
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
     assert rvz.LeafEvaluator(net, kernel="h2").accepts_live_count is True
-    assert rvz.LeafEvaluator(net, kernel="miopen").accepts_live_count is False
-    assert rvz.LeafEvaluator(net, kernel="resnet").accepts_live_count is False
+    assert make_evaluator(net, "miopen").accepts_live_count is False
+    assert make_evaluator(net, "resnet").accepts_live_count is False
 
 
 # measured on MI355X (r02): under both GPU evaluators, with no injection, both
@@ -108,7 +110,7 @@ def test_trajectory_agreement_with_reference_s800(kernel):
     G = len(games)
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, int(fx["blocks"]), int(fx["filters"])).cuda().eval()
-    ev = rvz.LeafEvaluator(net, kernel=kernel)
+    ev = make_evaluator(net, kernel)
     eng = rvz.Engine(G, num_simulations=int(fx["sims"]), batch_size=int(fx["batch"]),
                      c_puct=float(fx["c_puct"]))
     eng.reset([g["seed"] for g in games])
@@ -211,7 +213,7 @@ def test_h2_fp32_class_on_trained_weights(tmp_path):
     l64, v64 = _fp64_outputs(net, x)
     err, verr = {}, {}
     for kern in ("h2", "resnet"):
-        ev = rvz.LeafEvaluator(net, kernel=kern)
+        ev = make_evaluator(net, kern)
         lo, vo = ev(x)
         err[kern] = (lo.double().cpu() - l64).abs().max().item()
         verr[kern] = (vo.double().cpu() - v64).abs().max().item()

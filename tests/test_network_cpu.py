@@ -3,6 +3,7 @@ state_dict compatibility (same keys/shapes, TorchScript duplicates tolerated) an
 import os
 
 import numpy as np
+import pytest
 import torch
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "net_tiny.npz")
@@ -30,16 +31,28 @@ def test_state_dict_compatible_and_outputs_match():
     np.testing.assert_allclose(value.numpy(), d["value"], rtol=1e-5, atol=1e-6)
 
 
-def test_leaf_evaluator_folded_bn_cpu():
+def test_folded_bn_cpu():
+    """BN folding + the NHWC head-weight permutation (rvz.network._fold, the packed layout's
+    source) on the CPU, through the PyTorch alternative of tools/alt."""
     import rvz
+    from alt_eval import AltEvaluator
     d, sd = _load()
     net = rvz.AlphaZeroNetwork(8, 1, 16)
     net.load_state_dict(sd)
-    ev = rvz.LeafEvaluator(net, dtype=torch.float32, device="cpu")
+    ev = AltEvaluator(net, kernel="miopen", dtype=torch.float32, device="cpu")
     logits, value = ev(torch.from_numpy(d["x"]))
     np.testing.assert_allclose(logits.numpy(), d["logits"], rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(value.numpy(), d["value"], rtol=1e-4, atol=1e-5)
     assert ev.flops_per_row() > 0
+
+
+def test_leaf_evaluator_has_no_cpu_fallback():
+    import rvz
+    net = rvz.AlphaZeroNetwork(8, 1, 64)
+    with pytest.raises(rvz.RvzError):
+        rvz.LeafEvaluator(net, device="cpu")
+    with pytest.raises(ValueError):
+        rvz.LeafEvaluator(net, kernel="miopen")
 
 
 def fixture_planes(path, n=None):

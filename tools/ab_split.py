@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "alphazero-reversi_amd"))
 import rvz  # noqa: E402
 from rvz import _lib  # noqa: E402
 
-src = os.path.join(ROOT, "alphazero-reversi_amd", "csrc", "rvz_resnet.hip")
+src = os.path.join(ROOT, "tools", "alt", "rvz_resnet_alt.hip")
 variants = []
 for item in os.environ.get("RVZ_AB", "base:").split(";"):
     name, flags = item.split(":", 1)
@@ -35,7 +35,9 @@ for item in os.environ.get("RVZ_AB", "base:").split(";"):
 blocks, filters, n = (int(a) for a in (sys.argv[1:4] if len(sys.argv) > 3 else (6, 64, 4096)))
 torch.manual_seed(0)
 net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
-ev = rvz.LeafEvaluator(net, kernel="split")
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt"))
+from alt_eval import AltEvaluator  # noqa: E402
+ev = AltEvaluator(net, kernel="split")
 x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
 lg = torch.empty(n, 65, device="cuda")
 v = torch.empty(n, device="cuda")

@@ -1,4 +1,4 @@
-// rvz_nn.hip — leaf-evaluator helpers for the policy/value ResNet.
+// rvz_nn_alt.hip (tools/alt/librvz_alt.so, the MIOpen evaluator's A/B path) — leaf-evaluator helpers for the policy/value ResNet.
 //
 // MIOpen's NHWC fp32 implicit-GEMM convolution runs at ~85% of the fp32 MFMA peak on the C2 shape,
 // but PyTorch then spends three more full passes over every activation: the conv bias add, the
@@ -10,7 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "../../include/rvz.h"
+#include "rvz_alt.h"
 
 namespace {
 

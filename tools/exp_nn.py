@@ -12,7 +12,10 @@ import torch.nn.functional as F
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "alphazero-reversi_amd"))
-import rvz  # noqa: E402
+import rvz
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "alt"))
+from alt_eval import AltEvaluator  # noqa: E402
 
 
 def timeit(fn, x, iters=20):
@@ -55,7 +58,7 @@ def main():
     for bench_mode in (False, True):
         torch.backends.cudnn.benchmark = bench_mode
         for dtype in (torch.float32, torch.bfloat16):
-            ev = rvz.LeafEvaluator(net, dtype=dtype)
+            ev = AltEvaluator(net, kernel="miopen", dtype=dtype)
             key = f"nhwc_{'fp32' if dtype == torch.float32 else 'bf16'}_bench{int(bench_mode)}"
             res[key] = round(graph_time(ev, x), 4)
         with torch.no_grad():

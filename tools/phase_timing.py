@@ -32,8 +32,8 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
     kern = os.environ.get("KERNEL", "h2")
-    ev = rvz.LeafEvaluator(net, kernel=kern)
-    fwd = lib.rvz_resnet_fwd_h2 if kern == "h2" else lib.rvz_resnet_fwd_split
+    ev = rvz.LeafEvaluator(net)  # h2 (the split kernel is in tools/alt)
+    fwd = lib.rvz_resnet_fwd_h2
     x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
     lg = torch.empty(n, 65, device="cuda")
     wk = torch.zeros(n * 192 + 4, device="cuda")
