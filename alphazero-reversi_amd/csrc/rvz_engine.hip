@@ -22,8 +22,9 @@
 //    balanced tree), so u = c*P*sqrt(Np) / (1 + N).
 //  * value_sum is float32 (NumPy>=2 promotion of the np.float32 NN value); terminal values are
 //    small integers, exact in float32, so one float32 accumulator reproduces the Python mix.
-//  * sqrt(Np) is (float)sqrt((double)n) computed on the device: gfx950's f64 sqrt is correctly
-//    rounded (tests/test_gpu_numerics.py), so it equals math.sqrt then the float32 cast.
+//  * sqrt(Np) is the correctly rounded f32 sqrt of (float)n (sqrt_count): equal to math.sqrt in
+//    double then the float32 cast (double rounding through >= 2p + 2 bits is innocuous for
+//    sqrt; tests/test_gpu_numerics.py checks every n <= 4,000,000), at f32 cost.
 #include <hip/hip_bf16.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -36,6 +37,7 @@
 
 #include "../../include/rvz.h"
 #include "rvz_rules.hip.h"
+#include "rvz_trace.h"
 
 using namespace rvz;
 
@@ -213,8 +215,14 @@ __device__ __forceinline__ int backup_path(Node* nodes, int path_reg, int plen, 
 }
 
 // UCB of an expanded child whose score is not cached (mcts.py:102-114); turn_c = child's turn.
-// sqrt: the device f64 sqrt is correctly rounded (tests/test_gpu_numerics.py), so this is
-// exactly `np.float32(math.sqrt(parent_visit_count))` as the reference's NumPy promotion takes it.
+// sqrt_np = sqrt_count(parent N): exactly `np.float32(math.sqrt(parent_visit_count))` as the
+// reference's NumPy promotion takes it.
+// np.float32(math.sqrt(n)) for a visit count n < 2^24: math.sqrt rounds the exact root to 53
+// bits, the cast to 24; rounding twice through p' >= 2p + 2 bits (53 >= 50) equals rounding once
+// for sqrt (Figueroa), so the correctly rounded f32 sqrt of (float)n (exact for n < 2^24) is the
+// same value (-fhip-fp32-correctly-rounded-divide-sqrt; tests/test_gpu_numerics.py)
+__device__ __forceinline__ float sqrt_count(int n) { return __builtin_sqrtf((float)n); }
+
 __device__ __forceinline__ float ucb_score(const Node& c, float sqrt_np, int turn_c, float cpuct) {
     float u = cpuct * c.p;
     u = u * sqrt_np;
@@ -391,7 +399,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                     } else if (!isnan(c.c)) {
                         score = c.c;
                     } else {
-                        const float sq_np = (float)sqrt((double)parent_n);
+                        const float sq_np = sqrt_count(parent_n);
                         score = ucb_score(c, sq_np, 3 - m_turn(m), v.cpuct);
                         nodes[base + lane].c = score;
                         wrote = true;
@@ -453,7 +461,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                     if (lane >= 1 && lane <= depth && fp_b >= 0) {
                         Node cn;
                         cn.n = fn; cn.w = fw; cn.p = fpr; cn.c = 0.0f;
-                        const float sc = ucb_score(cn, (float)sqrt((double)par_n), fp_turn,
+                        const float sc = ucb_score(cn, sqrt_count(par_n), fp_turn,
                                                    v.cpuct);
                         const uint32_t ks = score_key(sc), kb = score_key(fp_sb);
                         hold = ks > kb || (ks == kb && fp_ci < fp_b);
@@ -1091,6 +1099,7 @@ int rvz_env_reset(rvz_engine* e, const uint32_t* seeds, const uint8_t* mask) {
 
 int rvz_env_autoreset(rvz_engine* e, const int32_t* idx, int64_t* seeds, int64_t stride,
                       int64_t* plies, int64_t* done, int32_t reset) {
+    const Range trace_range("rvz.env.autoreset");
     if (!e || !idx || !plies || (reset && (!seeds || !done))) return RVZ_EINVAL;
     if (reset) e->pending = 0;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);
@@ -1162,6 +1171,7 @@ int rvz_env_legal(rvz_engine* e, uint64_t* out) {
 }
 
 int rvz_env_apply(rvz_engine* e, const int32_t* sq, int32_t* ok) {
+    const Range trace_range("rvz.env.apply");
     if (!e) return RVZ_EINVAL;
     int r = rvz_board_apply(e->BS, e->v.G, e->v.black, e->v.white, e->v.status, sq, ok, e->stream);
     if (r != RVZ_OK) e->err = "rvz_env_apply launch failed";
@@ -1171,6 +1181,7 @@ int rvz_env_apply(rvz_engine* e, const int32_t* sq, int32_t* ok) {
 }
 
 int rvz_search_begin(rvz_engine* e) {
+    const Range trace_range("rvz.search.begin");
     if (!e) return RVZ_EINVAL;
     e->next_batch = 0;
     e->searching = 1;
@@ -1184,6 +1195,7 @@ int rvz_search_begin(rvz_engine* e) {
 }
 
 int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
+    const Range trace_range("rvz.search.step (expand/backup + select)");
     if (!e || !leaf_x || !need) return RVZ_EINVAL;
     if (!e->searching) { e->err = "rvz_search_step before rvz_search_begin"; return RVZ_EINVAL; }
     const int S = e->cfg.num_simulations, B = e->cfg.batch_size;
@@ -1215,6 +1227,7 @@ int rvz_search_step(rvz_engine* e, void* leaf_x, int32_t* need) {
 }
 
 int rvz_search_submit(rvz_engine* e, const float* policy, int32_t is_logits, const float* value) {
+    const Range trace_range("rvz.search.submit");
     if (!e || !policy || !value) return RVZ_EINVAL;
     if (!e->searching || e->next_batch == 0) {
         e->err = "rvz_search_submit without a preceding rvz_search_step";
@@ -1350,6 +1363,7 @@ int rvz_search_skip(rvz_engine* e) {
 
 int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, int32_t* out_idx,
             double* out_p) {
+    const Range trace_range("rvz.act (expand/backup + action + move)");
     if (!e || !out_idx || !out_p) return RVZ_EINVAL;
     const int ex = e->pending;
     dim3 grid(grid_games(e->v.G)), block(WPB * WAVE);

@@ -10,6 +10,7 @@
 // The A/B alternatives (exact f32 MFMA, 3-part bf16 split, VALU heads, the MIOpen epilogue) are
 // built into tools/alt/librvz_alt.so, not into this library.
 #include "rvz_resnet_common.hip.h"
+#include "rvz_trace.h"
 
 namespace {
 
@@ -723,6 +724,7 @@ int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n
 int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const float* params,
                            int32_t filters, int32_t blocks, float* logits, float* value,
                            const int32_t* n_live, uint32_t* stamp_ctr, void* stream) {
+    const rvz::Range trace_range("rvz.eval.heads (k_heads_mfma)");
     if (!work || !params || !logits || !value || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128))
         return RVZ_EINVAL;
@@ -769,6 +771,7 @@ int rvz_resnet_trunk_h2_ex(int32_t board, const float* x, int32_t n, const float
                            const uint16_t* blob, int32_t filters, int32_t blocks, float* work,
                            const int32_t* n_live, uint64_t* stamps, const uint32_t* stamp_ctr,
                            int32_t ring, void* stream) {
+    const rvz::Range trace_range("rvz.eval.trunk (k_resnet_h2)");
     if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128) || (stamp_ctr && (!stamps || ring <= 0)))
         return RVZ_EINVAL;

@@ -287,7 +287,7 @@ def cpu_baseline(args, net):
     try:
         gomp = ctypes.CDLL("libgomp.so.1")
         gomp.omp_set_num_threads(1)
-        G1 = 48
+        G1 = min(48, G)
         stub1 = O.Search(G1, args.sims, args.batch, 1.0, bs=args.board)
         t2 = time.perf_counter()
         stub1.begin([O.new_game(args.board) for _ in range(G1)])

@@ -6,8 +6,22 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+def test_sqrt_count_equals_math_sqrt_then_f32():
+    """k_step's sqrt_count(N) (correctly rounded f32 sqrt of (float)N, built with the product's
+    flags in tools/alt) == np.float32(math.sqrt(N)), the reference's UCB term, for every N up to
+    4,000,000."""
+    import alt_eval
+    from rvz import _lib
+    n = 4_000_001
+    out = torch.empty(n, device="cuda")
+    _lib.check(alt_eval.load().rvz_alt_sqrt_count(n, out.data_ptr(), _lib.stream_handle()),
+               None, "rvz_alt_sqrt_count")
+    ref = np.sqrt(np.arange(n, dtype=np.float64)).astype(np.float32)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
 def test_device_f64_sqrt_correctly_rounded_then_f32():
-    """k_step takes (float)sqrt((double)N) on the device for the UCB's math.sqrt(parent N)."""
+    """The f64 sqrt on the device is correctly rounded (the k_act power path's sqrt, T = 2)."""
     n = np.arange(0, 4_000_001, dtype=np.float64)
     dev = torch.sqrt(torch.from_numpy(n).cuda()).cpu().numpy()
     assert np.array_equal(dev, np.sqrt(n))

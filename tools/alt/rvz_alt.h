@@ -40,6 +40,9 @@ int rvz_alt_heads_valu(int32_t board, const float *work, int32_t n, const float 
                        int32_t filters, int32_t blocks, float *logits, float *value,
                        void *hip_stream);
 
+/* out[i] = the engine's sqrt_count(i) (csrc/rvz_engine.hip) for i < n, same compile flags. */
+int rvz_alt_sqrt_count(int32_t n, float *out, void *hip_stream);
+
 #ifdef __cplusplus
 }
 #endif
