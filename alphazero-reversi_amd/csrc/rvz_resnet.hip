@@ -195,13 +195,20 @@ struct H2W {
     }
 };
 // f16x8 index of k-step `it` of a layer (it >= NIT: the next layer's) from the layer's base:
-// [tap][kstep][part][ctile][lane]. mirror: the wave walks the taps as 8 - t (ILV pixel group 1:
-// dr, dc -> -dr, -dc), so both groups meet their edge taps at the same it.
+// [tap][kstep][part][ctile][lane]. mirror (ILV pixel group 1): the wave walks the tap rows in
+// reverse, so both groups meet their edge taps at the same it.
+#ifndef RVZ_H2_MIRROR
+#define RVZ_H2_MIRROR 2      // 1: (dr, dc) -> (-dr, -dc); 2: rows only, (dr, dc) -> (-dr, dc)
+#endif
+// the natural tap a mirrored wave reads at iteration tap t
+__host__ __device__ constexpr int h2_mirror_tap(int t) {
+    return RVZ_H2_MIRROR == 1 ? 8 - t : (2 - t / 3) * 3 + t % 3;
+}
 template <int F>
 __device__ __forceinline__ int h2_frag(int it, bool mirror) {
     constexpr int KS = F / H2_K, NIT = 9 * KS, CT = F / H2_TM, KSTEP = 2 * CT * 64;
     const int lay = it / NIT, itn = it % NIT, t = itn / KS, ks = itn % KS;
-    const int tn = mirror ? 8 - t : t;
+    const int tn = mirror ? h2_mirror_tap(t) : t;
     return (lay * NIT + tn * KS + ks) * KSTEP;
 }
 
@@ -379,12 +386,13 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     using C = CfgH<F, G::NPIX>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
     // ILV: tile 0 is board row 0 (pixel group 0) or row 7 (group 1), and the taps with dr = -1
-    // (row 0) or dr = +1 (row 7) leave the boards for all its pixels. Group 1 walks the taps
-    // mirrored (8 - t), so both groups skip tile 0's A loads and MFMAs in k-steps [0, SKIP), a
-    // compile-time window. Measured (tools/ab_h2.py, one box, C2 trunk): -1.9%; the mirrored
-    // order alone costs +3.3% (the two waves of a channel group no longer fetch the same weight
-    // fragments together: more L2 traffic, a lower clock), the skip saves 5%. Instantiating the
-    // k-loop once per group instead (both in natural order) spilled 74 VGPRs.
+    // (row 0) or dr = +1 (row 7) leave the boards for all its pixels. Group 1 walks the tap rows
+    // in reverse (dr -> -dr, RVZ_H2_MIRROR 2), so both groups skip tile 0's A loads and MFMAs in
+    // k-steps [0, SKIP), a compile-time window, and still fetch the same weight fragments
+    // together in the middle row (dr = 0). Measured (tools/ab_h2.py, one box, C2 trunk): -3.2%
+    // against no skip (profiles/r02k_ab_h2_mirror_c2.json); the full mirror (dr, dc -> -dr, -dc)
+    // shares only the centre tap: -2.1%. Instantiating the k-loop once per group instead (both
+    // in natural order) spilled 74 VGPRs.
     constexpr int SKIP = ILV ? 3 * KS : 0;
     const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
     const bool mirror = ILV && wave / WaveTilesH<F, CTW, PTW>::CG != 0;
@@ -394,7 +402,9 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
 #pragma unroll
     for (int u = 0; u < PTW; ++u) {
         const unsigned m = G::taps(wt.px[u]);
-        pmask[u] = mirror ? __builtin_bitreverse32(m) >> 23 : m;
+        pmask[u] = !mirror ? m
+                   : RVZ_H2_MIRROR == 1 ? __builtin_bitreverse32(m) >> 23
+                                        : ((m & 7u) << 6) | (m & 0x38u) | ((m >> 6) & 7u);
     }
     f32x4 acc[CTW][PTW];
 #pragma unroll
@@ -411,7 +421,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     };
     auto load_a = [&](f16x8 (&aq)[PTW][2], int it) {
         const int t = it / KS, ks = it - t * KS;
-        const int off = mirror ? -G::tap_offset(t) : G::tap_offset(t);
+        const int off = mirror ? G::tap_offset(h2_mirror_tap(t)) : G::tap_offset(t);
 #pragma unroll
         for (int u = (it < SKIP ? 1 : 0); u < PTW; ++u) {
             const int nat = wt.px[u] + off;
