@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU round with the extra configurations: parity tests, smoke, C2 bench + rocprof kernel stats,
-# C3 (1 and 2 lanes, 60 plies), C1. Each GPU step has its own time limit; a crash or timeout
+# C3 (1 and 2 lanes, 60 plies), C1, C5. Each GPU step has its own time limit; a crash or timeout
 # (exit > 1) ends the script there. Outputs under gpurun_out/ with the given TAG.
 set -u
 OUT=${OUT:-gpurun_out}
@@ -25,5 +25,6 @@ if [ -z "${SKIP_EXTRA:-}" ]; then
 step bench_c3 400 python bench.py --config c3 --no-cpu-baseline > "$OUT/bench_c3_$TAG.json" 2> "$OUT/bench_c3_$TAG.err"
 step bench_c3_l2 400 python bench.py --config c3 --lanes 2 --no-cpu-baseline > "$OUT/bench_c3l2_$TAG.json" 2> "$OUT/bench_c3l2_$TAG.err"
 step bench_c1 300 python bench.py --config c1 > "$OUT/bench_c1_$TAG.json" 2> "$OUT/bench_c1_$TAG.err"
+step bench_c5 300 python bench.py --config c5 --no-cpu-baseline > "$OUT/bench_c5_$TAG.json" 2> "$OUT/bench_c5_$TAG.err"
 fi
 echo round-done
