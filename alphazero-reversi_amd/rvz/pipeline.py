@@ -35,7 +35,8 @@ class SelfPlayTrainer:
                  c_puct: float = 1.0, temperature: float = 1.0, seed: int = 42,
                  train_steps: Optional[int] = None, train_batch: int = 64, lr: float = 1e-3,
                  weight_decay: float = 1e-4, gradient_clip: float = 1.0,
-                 graph: bool = True, compact_leaves: bool = True):
+                 graph: bool = True, compact_leaves: bool = True, lr_milestones=(),
+                 lr_gamma: float = 0.1):
         self.model = model.eval()
         self.device = next(model.parameters()).device
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -44,7 +45,8 @@ class SelfPlayTrainer:
         self.games, self.seed = int(games), int(seed)
         self.train_steps = train_steps
         self.trainer = DDPTrainer(model, lr=lr, weight_decay=weight_decay,
-                                  gradient_clip=gradient_clip, batch_size=train_batch)
+                                  gradient_clip=gradient_clip, batch_size=train_batch,
+                                  lr_milestones=lr_milestones, lr_gamma=lr_gamma)
         self.evaluator = LeafEvaluator(model)
         bs = int(getattr(model, "board_size", 8))
         self.eng = Engine(games, num_simulations, batch_size, c_puct, board_size=bs,
@@ -83,6 +85,7 @@ class SelfPlayTrainer:
         out = self.trainer.train_epoch(data, seed=self.seed + self.iteration,
                                        max_steps=self.train_steps, local_data=True)
         self.trainer.sync_buffers()
+        self.trainer.scheduler_step()          # pipeline.py:131, once per iteration
         self.model.eval()
         self.evaluator.refresh()
         return out

@@ -59,7 +59,11 @@ def records_to_training(rec_black: torch.Tensor, rec_white: torch.Tensor, rec_si
 class DDPTrainer:
     def __init__(self, model: nn.Module, lr: float = 1e-3, weight_decay: float = 1e-4,
                  gradient_clip: float = 1.0, policy_loss_weight: float = 1.0,
-                 value_loss_weight: float = 1.0, batch_size: int = 64, bucket_cap_mb: int = 25):
+                 value_loss_weight: float = 1.0, batch_size: int = 64, bucket_cap_mb: int = 25,
+                 lr_milestones=(), lr_gamma: float = 0.1):
+        """Defaults = the reference's TrainingConfig (config.py:46-60): AdamW(lr 1e-3, weight decay
+        1e-4), clip 1.0, loss weights 1, batch 64, MultiStepLR(milestones [], gamma 0.1)
+        (pipeline.py:91-105), stepped once per iteration (scheduler_step, pipeline.py:131)."""
         self.model = model
         self.device = next(model.parameters()).device
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -71,6 +75,8 @@ class DDPTrainer:
         else:
             self.net = model
         self.opt = torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay)
+        self.scheduler = torch.optim.lr_scheduler.MultiStepLR(self.opt, milestones=list(lr_milestones),
+                                                              gamma=lr_gamma)
         self.clip = gradient_clip
         self.wp, self.wv = policy_loss_weight, value_loss_weight
         self.batch_size = batch_size
@@ -84,6 +90,10 @@ class DDPTrainer:
             return
         for b in self.model.buffers():
             dist.broadcast(b, 0)
+
+    def scheduler_step(self):
+        """The per-iteration learning-rate step of the reference's train loop (pipeline.py:131)."""
+        self.scheduler.step()
 
     def rank_world(self):
         return (dist.get_rank(), dist.get_world_size()) if self.distributed else (0, 1)
@@ -111,15 +121,23 @@ class DDPTrainer:
         holds its own data (its own self-play games, rvz.pipeline) and walks its own permutation
         (seed + rank). Either way each step's global batch is world x batch_size, and every rank
         runs the same number of steps (the minimum over ranks). Returns the reference's averaged
-        loss dict (pipeline.py:342-366)."""
+        loss dict (pipeline.py:342-366).
+        Order: the permutation the reference's DataLoader(shuffle=True) draws when handed a
+        generator seeded with `seed` (its base-seed draw, then randperm(n)). On one
+        process the last partial batch is trained too, as the reference's DataLoader (no
+        drop_last) does; across ranks every step is a full world x batch_size batch."""
         rank, world = self.rank_world()
         n = data["states"].shape[0]
         g = torch.Generator().manual_seed(seed + (rank if local_data else 0))
+        # DataLoader(shuffle=True, generator=g) first draws its workers' base seed from g, then
+        # the RandomSampler's permutation: the same two draws give the same batches
+        torch.empty((), dtype=torch.int64).random_(generator=g)
         order = torch.randperm(n, generator=g)
         if local_data:
             rank, world = 0, 1        # indexing within this rank's own permutation
         per_step = self.batch_size * world
-        steps = n // per_step
+        partial = not self.distributed and world == 1
+        steps = -(-n // per_step) if partial else n // per_step
         if max_steps is not None:
             steps = min(steps, max_steps)
         if self.distributed:          # every rank must run the same number of DDP steps
