@@ -546,6 +546,8 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         const int plane = i / (8 * H2_K), k = i % (8 * H2_K);
         actA[plane * C::KSP + C::ZROW * H2_K + k] = 0;
     }
+    // (issuing the stem's loads before the first conv's weight prefetch measured neutral: the
+    // stem's epilogue time is the partner workgroup's MFMAs sharing the SIMD, not a load wait)
     const H2W wr(blob, h2_blob_elems(F, n_blocks));
     f16x8 bc[RVZ_H2_PD][CTW][2];
     if (n_blocks > 0) {

@@ -19,7 +19,8 @@ import rvz  # noqa: E402
 from rvz import _lib  # noqa: E402
 
 EXTRA = [f for f in os.environ.get("RVZ_PHASE_FLAGS", "").split() if f]
-SO = "/tmp/librvz_phase%s.so" % "".join(EXTRA).replace("-", "_").replace("=", "")
+SO = os.environ.get("RVZ_PHASE_SO") or \
+    "/tmp/librvz_phase%s.so" % "".join(EXTRA).replace("-", "_").replace("=", "")
 src = os.path.join(ROOT, "alphazero-reversi_amd", "csrc")
 if not os.path.exists(SO):
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
