@@ -254,6 +254,46 @@ def test_c3_workload_two_plies(oracle):
     assert not ev.overflowed()
 
 
+def test_c5_workload_two_plies(oracle):
+    """C5 as configured (BASELINE.json configs[4]): 16,384 6x6 games x 400 sims with the 6x64 h2
+    evaluator on packed 6x6 boards, compacted leaf batches, two plies: no device error or
+    overflow, every move legal, and 16 sampled games' visits and moves equal the literal oracle
+    search fed by the same evaluator (parity of the 6x6 variant is unpinned by design: the
+    reference's Board rejects size != 8, board.py:27-28; the oracle generalises its rules)."""
+    import rvz
+    G, S, BS = 16384, 400, 6
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(BS, 6, 64).cuda().eval()
+    ev = rvz.LeafEvaluator(net)
+    eng = rvz.Engine(G, num_simulations=S, batch_size=64, board_size=BS, compact_leaves=True)
+    eng.reset(range(G))
+    sample = np.linspace(0, G - 1, 16).astype(int)
+    games = [oracle.new_game(BS) for _ in sample]
+    mts = [oracle.MT(int(g)) for g in sample]
+    for ply in range(2):
+        b0, w0, st0 = (t.clone() for t in eng.get_state())
+        eng.search(ev, fused_softmax=False)          # torch's F.softmax on both sides
+        vis = eng.visits().cpu().numpy().copy()
+        idx, _ = eng.act(1.0, apply=True)
+        idx = idx.cpu().numpy()
+        eng.check()
+        legal = rvz.board_legal(b0, w0, st0, BS).cpu().numpy().view(np.uint64)
+        assert all((int(legal[g]) >> int(idx[g])) & 1 for g in range(G))
+        srch = oracle.Search(len(sample), S, 64, 1.0, bs=BS)
+        srch.begin(games)
+        while (r := srch.step()) is not None:
+            x = torch.from_numpy(oracle.leaf_planes(r[0], BS)).cuda()
+            lo, vo = ev(x)
+            srch.submit(torch.softmax(lo, 1).cpu().numpy(), vo.cpu().numpy())
+        ov = srch.visits()
+        assert np.array_equal(ov, vis[sample]), ply
+        for j, g in enumerate(sample):
+            a, _, _ = oracle.action(ov[j], 1.0, mts[j].random_sample())
+            assert a == idx[g]
+            assert oracle.make_move(games[j], a, BS)
+    assert not ev.overflowed()
+
+
 def test_bf16_leaf_planes_equal_f32():
     import rvz
     G = 512

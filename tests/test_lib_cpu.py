@@ -80,3 +80,20 @@ def test_trunk_stamp_decoding():
     assert trunk_spans(st, 0) is None
     full = trunk_spans(st[:2], 7)         # wrapped: both rows kept
     assert full["launches"] == 7 and full["rows"] == 3.5
+
+
+def test_alt_library_matches_its_header():
+    """tools/alt/librvz_alt.so (the A/B and cross-check build) exports exactly what
+    tools/alt/rvz_alt.h declares, its ctypes table covers the header, and the product library
+    exports none of it (the alternatives are not on the product surface)."""
+    import alt_eval
+    hdr = open(os.path.join(ROOT, "tools", "alt", "rvz_alt.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    decl = set(re.findall(r"\b(rvz_[a-z0-9_]+)\s*\(", hdr))
+    assert set(alt_eval.SIGNATURES) == decl
+    out = subprocess.run(["nm", "-D", "--defined-only", alt_eval.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (rvz_[a-z0-9_]+)", out))
+    assert exported == decl, exported ^ decl
+    alt_eval.load()
+    assert not decl & set(declared_symbols())
