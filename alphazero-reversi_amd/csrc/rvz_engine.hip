@@ -633,7 +633,9 @@ __device__ __forceinline__ double np_power(double x, double e) {
 // act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action); optionally preceded
 // by the last batch's pending expand + backup.
 template <int BS>
-__global__ __launch_bounds__(256) void k_act(View v, int expand, const float* __restrict__ policy,
+// 8x8: <= 80 VGPRs (6 waves per SIMD), so a k_act wave fits on a SIMD beside two trunk waves
+// (2 x 216); the 6x6 form would spill under that cap
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? 6 : 1))) void k_act(View v, int expand, const float* __restrict__ policy,
                                              int is_logits, const float* __restrict__ value,
                                              double temperature, const double* __restrict__ uo,
                                              int apply, int32_t* __restrict__ out_idx,

@@ -212,11 +212,15 @@ __device__ __forceinline__ int h2_frag(int it, bool mirror) {
     return (lay * NIT + tn * KS + ks) * KSTEP;
 }
 
-// RVZ_H2_SKIP_LDS 1: the skip input is re-read from LDS as its two parts (x0 + x1, 22 bits) at
-// the place conv B overwrites, instead of kept in 32 fp32 registers (frees them for a deeper
-// weight prefetch; no measurable error change, tools/emu_split.py f16x2_1acc_lds)
+// RVZ_H2_SKIP_LDS 1 (default): the skip input is re-read from LDS as its two parts (x0 + x1,
+// 22 bits: the precision the conv inputs already carry; no measurable error change,
+// tools/emu_split.py f16x2_1acc_lds) at the place conv B overwrites it, instead of kept in 32
+// fp32 registers. The trunk then needs 216 VGPRs instead of 248, so a k_step or k_act wave (80)
+// fits on a SIMD beside the two trunk waves (2 x 216 + 80 = 512) instead of taking a trunk
+// workgroup's place: the kernel alone is ~1.4% slower, the whole C2 ply 0.9% faster (one-box
+// bench A/B, profiles/r02s_ablib_skiplds.txt).
 #ifndef RVZ_H2_SKIP_LDS
-#define RVZ_H2_SKIP_LDS 0
+#define RVZ_H2_SKIP_LDS 1
 #endif
 template <int CTW, int PTW>
 struct EpiH {
@@ -494,8 +498,15 @@ struct XinStage {
     }
 };
 
+// RVZ_H2_MAXV (experiments): cap the trunk's VGPRs so that a k_step wave (80) fits on a SIMD
+// beside two trunk waves (2 x 216 + 80 = 512)
+#ifdef RVZ_H2_MAXV
+#define RVZ_H2_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RVZ_H2_MAXV)))
+#else
+#define RVZ_H2_VGPR_ATTR
+#endif
 template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) RVZ_H2_VGPR_ATTR
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, const int32_t* __restrict__ n_live,
