@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../../include/rvz.h"
+#include "rvz_pow.hip.h"
 #include "rvz_rules.hip.h"
 #include "rvz_trace.h"
 
@@ -620,14 +621,15 @@ __global__ __launch_bounds__(256) void k_visits(View v, int32_t* __restrict__ ou
     if (lane == 0) out[(size_t)g * NPOL + NSQ] = 0;  // no pass child is ever created
 }
 
-// numpy `arr ** e` for float64 (fast_scalar_power paths, else pow).
+// numpy `arr ** e` for float64 (fast_scalar_power paths, else the correctly rounded power; NumPy's
+// general power is host-dependent, csrc/rvz_pow.hip.h)
 __device__ __forceinline__ double np_power(double x, double e) {
     if (e == 1.0) return x;
     if (e == 2.0) return x * x;
     if (e == 0.5) return sqrt(x);
     if (e == -1.0) return 1.0 / x;
     if (e == 0.0) return 1.0;
-    return pow(x, e);
+    return rvz_pow::pow_cr(x, e);
 }
 
 // act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action); optionally preceded

@@ -44,6 +44,8 @@ SIGNATURES = {
     "rvz_alt_heads_valu": (C.c_int, [C.c_int32, _P, C.c_int32, _P, C.c_int32, C.c_int32, _P, _P,
                                      _P]),
     "rvz_alt_sqrt_count": (C.c_int, [C.c_int32, _P, _P]),
+    "rvz_alt_pow": (C.c_int, [C.c_int32, _P, _P, _P, C.c_int32, _P]),
+    "rvz_alt_pow_host": (C.c_int, [C.c_int32, _P, _P, _P]),
 }
 _alt = None
 

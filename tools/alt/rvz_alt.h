@@ -42,6 +42,11 @@ int rvz_alt_heads_valu(int32_t board, const float *work, int32_t n, const float 
 
 /* out[i] = the engine's sqrt_count(i) (csrc/rvz_engine.hip) for i < n, same compile flags. */
 int rvz_alt_sqrt_count(int32_t n, float *out, void *hip_stream);
+/* out[i] = x[i] ** e[i] in float64: mode 1 = k_act's correctly rounded power (csrc/rvz_pow.hip.h),
+ * mode 0 = the device library's pow; rvz_alt_pow_host = the same pow_cr compiled for the host. */
+int rvz_alt_pow(int32_t n, const double *x, const double *e, double *out, int32_t mode,
+                void *hip_stream);
+int rvz_alt_pow_host(int32_t n, const double *x, const double *e, double *out);
 
 #ifdef __cplusplus
 }
