@@ -128,13 +128,27 @@ __device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int
 // g = lane >> 4), so a lane loads 4 consecutive k of its weight row (f32x4, L2) and of its
 // board's input row (ds_read_b128) per 4 MFMAs. Value fc2 (256 -> 1) + tanh reduce the fc1 tiles
 // through registers, lane shuffles and 64 floats of LDS.
+// RVZ_HEADS_STREAM 1 (default): the weight fragments are streamed through buffer loads,
+// RVZ_HEADS_PD steps (one f32x4 and 4 MFMAs each) ahead, instead of all held at once (148 VGPRs).
+// The kernel then fits in 76 VGPRs, so its waves run beside two trunk waves (2 x 216) instead of
+// waiting for a trunk workgroup to end: C2 +0.3% (3 alternating whole-bench pairs, 727.0k ->
+// 729.5k, profiles/r02z_ab_heads.txt; PD 6+ spills under the 80-VGPR cap).
+#ifndef RVZ_HEADS_STREAM
+#define RVZ_HEADS_STREAM 1
+#endif
+#ifndef RVZ_HEADS_PD
+#define RVZ_HEADS_PD 4
+#endif
+#if RVZ_HEADS_STREAM
+#define RVZ_HEADS_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#else
+#define RVZ_HEADS_ATTR
+#endif
 template <int BS>
-__global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ work, int n,
-                                                    const float* __restrict__ prm, Layout L,
-                                                    float* __restrict__ logits,
-                                                    float* __restrict__ value,
-                                                    const int32_t* __restrict__ n_live,
-                                                    uint32_t* __restrict__ stamp_ctr) {
+__global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
+    const float* __restrict__ work, int n, const float* __restrict__ prm, Layout L,
+    float* __restrict__ logits, float* __restrict__ value, const int32_t* __restrict__ n_live,
+    uint32_t* __restrict__ stamp_ctr) {
     // bench.py: the trunk launch before this one is complete; advance its stamp ring
     if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
     if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
@@ -147,6 +161,36 @@ __global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ wo
     __shared__ float vpart[4][16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int g0 = blockIdx.x * 16, col = lane & 15, grp = lane >> 4;
+#if RVZ_HEADS_STREAM
+    // the wave's weight steps in order: value fc1 tiles wave + 4m (VJ steps each), then policy
+    // tiles wave + 4m (PJ steps each); step s = one f32x4 of the A row (unit 16 t + col,
+    // k = 16 j + 4 grp .. +3)
+    constexpr int NSV = VTW * VJ, NS = NSV + PTW * PJ, D = RVZ_HEADS_PD < NS ? RVZ_HEADS_PD : NS;
+    // buffer loads: the lane's part of the address is one VGPR, the step's part (wave-uniform) the
+    // scalar soffset, so no 64-bit address per step is kept live
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc((void*)prm, (short)0, (int)(L.total * 4), 0x00020000);
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    auto load_step = [&](int s) -> f32x4 {
+        if (s < NSV) {
+            const int m = s / VJ, j = s % VJ;
+            const int so = (int)(L.vfc1_w + (16 * (wv + 4 * m)) * CELLS + 16 * j) * 4;
+            return 16 * j + 4 * grp < CELLS
+                       ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rw, (col * CELLS + 4 * grp) * 4, so, 0))
+                       : f32x4{};
+        }
+        const int m = (s - NSV) / PJ, j = (s - NSV) % PJ, o = 16 * (wv + 4 * m) + col;
+        const int so = (int)(L.pfc_w + (16 * (wv + 4 * m)) * PIN + 16 * j) * 4;
+        return (o < POUT && 16 * j + 4 * grp < PIN)
+                   ? __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rw, (col * PIN + 4 * grp) * 4, so, 0))
+                   : f32x4{};
+    };
+    f32x4 wq[D];
+#pragma unroll
+    for (int s = 0; s < D; ++s) wq[s] = load_step(s);
+#else
     // every weight fragment of this wave's tiles, issued before anything waits: value fc1 tiles
     // wave + 4m, policy tiles wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
     f32x4 av[VTW][VJ], ap[PTW][PJ];
@@ -167,19 +211,90 @@ __global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ wo
             ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
                            ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
     }
-    for (int i = tid; i < 16 * (PK + VK); i += 256) {
-        const int b = i / (PK + VK), k = i % (PK + VK), g = g0 + b;
-        float v = 0.0f;
-        if (g < n) {
-            if (k < PIN) v = work[(size_t)g * 192 + k];
-            else if (k >= PK && k - PK < CELLS) v = work[(size_t)g * 192 + PIN + (k - PK)];
+#endif
+    {   // the 16 workspace rows into LDS, 16 B per load, all loads in flight before the stores
+        // (policy planes at k < PIN, the value plane at PK.., zeros between)
+        constexpr int RQ = (PK + VK) / 4, NQ = 16 * RQ / 256;
+        static_assert(16 * RQ % 256 == 0 && PK % 4 == 0 && ROW % 4 == 0, "whole float4 rounds");
+        f32x4 v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + 256 * q, b = i / RQ, k = 4 * (i % RQ);
+            const int src = k < PIN ? k : (k >= PK && k - PK < CELLS ? PIN + k - PK : -1);
+            v[q] = g0 + b < n && src >= 0
+                       ? *reinterpret_cast<const f32x4*>(work + (size_t)(g0 + b) * 192 + src)
+                       : f32x4{};
         }
-        in[b * ROW + k] = v;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int i = tid + 256 * q, b = i / RQ, k = 4 * (i % RQ);
+            *reinterpret_cast<f32x4*>(in + b * ROW + k) = v[q];
+        }
     }
     __syncthreads();
     const float* inb = in + col * ROW + 4 * grp;
-    // value fc1 (+ bias, ReLU) and its fc2 partial
     float vp = 0.0f;
+#if RVZ_HEADS_STREAM
+    f32x4 acc = {};
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        __builtin_amdgcn_sched_barrier(0);   // keep each step's load in its step (no hoisting)
+        const f32x4 w = wq[s % D];
+        if (s + D < NS) wq[s % D] = load_step(s + D);
+        const bool val = s < NSV;
+        const int m = val ? s / VJ : (s - NSV) / PJ, j = val ? s % VJ : (s - NSV) % PJ;
+        const int t = wave + 4 * m;
+        if (j == 0) acc = f32x4{};
+        if (val || t < PT) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(inb + (val ? PK : 0) + 16 * j);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w[i], bx[i], acc, 0, 0, 0);
+        }
+        if (val && j == VJ - 1) {
+            // bias and fc2 weights of the tile's 4 rows: one 16-B buffer load each
+            const int ub = 16 * (wv + 4 * m);
+            const f32x4 b1 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                 rw, 16 * grp, (int)(L.vfc1_b + ub) * 4, 0));
+            const f32x4 w2 = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                 rw, 16 * grp, (int)(L.vfc2_w + ub) * 4, 0));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) vp = fmaf(fmaxf(acc[r] + b1[r], 0.0f), w2[r], vp);
+            if (m == VTW - 1) {
+                vp += __shfl_xor(vp, 16);
+                vp += __shfl_xor(vp, 32);
+                if (grp == 0) vpart[wave][col] = vp;
+            }
+        }
+        if (!val && j == PJ - 1 && t < PT) {
+            const f32x4 pb = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                 rw, 16 * grp, (int)(L.pfc_b + 16 * t) * 4, 0));
+            const int g = g0 + col;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int oo = 16 * t + 4 * grp + r;
+                if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + pb[r];
+            }
+        }
+    }
+#else
+    // value fc1 tile epilogue (+ bias, ReLU) into the fc2 partial
+    auto value_tile = [&](int m, const f32x4& acc) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {                // D row = unit 16t + 4grp + r, col = board
+            const int uu = 16 * (wave + 4 * m) + 4 * grp + r;
+            vp = fmaf(fmaxf(acc[r] + prm[L.vfc1_b + uu], 0.0f), prm[L.vfc2_w + uu], vp);
+        }
+    };
+    auto policy_tile = [&](int t, const f32x4& acc) {
+        const int g = g0 + col;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int oo = 16 * t + 4 * grp + r;
+            if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
+        }
+    };
+    // value fc1 (+ bias, ReLU) and its fc2 partial
 #pragma unroll
     for (int m = 0; m < VTW; ++m) {
         f32x4 acc = {};
@@ -190,11 +305,7 @@ __global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ wo
             for (int i = 0; i < 4; ++i)
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m][j][i], bx[i], acc, 0, 0, 0);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {                // D row = unit 16t + 4grp + r, col = board
-            const int uu = 16 * (wave + 4 * m) + 4 * grp + r;
-            vp = fmaf(fmaxf(acc[r] + prm[L.vfc1_b + uu], 0.0f), prm[L.vfc2_w + uu], vp);
-        }
+        value_tile(m, acc);
     }
     vp += __shfl_xor(vp, 16);
     vp += __shfl_xor(vp, 32);
@@ -212,13 +323,9 @@ __global__ __launch_bounds__(256) void k_heads_mfma(const float* __restrict__ wo
             for (int i = 0; i < 4; ++i)
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[m][j][i], bx[i], acc, 0, 0, 0);
         }
-        const int g = g0 + col;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int oo = 16 * t + 4 * grp + r;
-            if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
-        }
+        policy_tile(t, acc);
     }
+#endif
     __syncthreads();
     if (tid < 16 && g0 + tid < n)
         value[g0 + tid] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
