@@ -525,6 +525,9 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
     uint16_t* actB = actA + C::ACT;
     float* xin = reinterpret_cast<float*>(actB);     // free until the first conv writes B
+#ifdef RVZ_H2_PRIO   // experiments: trunk waves ahead of co-resident search waves in issue
+    __builtin_amdgcn_s_setprio(RVZ_H2_PRIO);
+#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g0 = blockIdx.x * NBOARD;
