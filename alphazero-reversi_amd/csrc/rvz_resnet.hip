@@ -511,7 +511,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, const int32_t* __restrict__ n_live,
                  uint64_t* __restrict__ stamps, const uint32_t* __restrict__ stamp_ctr,
-                 int ring) {
+                 int ring, uint32_t* __restrict__ claim) {
     using WT = WaveTilesH<F, CTW, PTW>;
     // row-interleaved pair of 8x8 boards (GeoH ILV): two pixel groups of 4 tiles = 8 board rows
     constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
@@ -530,7 +530,22 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
 #endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g0 = blockIdx.x * NBOARD;
+    int unit = blockIdx.x;
+    if (claim) {
+        // RVZ_H2_DYN: board units are dealt in workgroup start order from a counter in the
+        // workspace, over a grid larger than the units; the workgroups that start last (on the
+        // XCDs that run slowest) find none left and exit. The last of the grid's claims re-arms the
+        // counter for the next launch (stream order), so it is zero at every launch start.
+        __shared__ int s_unit;
+        if (tid == 0) {
+            const uint32_t u = atomicAdd(claim, 1u);
+            if (u == gridDim.x - 1) atomicExch(claim, 0u);
+            s_unit = (int)u;
+        }
+        __syncthreads();
+        unit = s_unit;
+    }
+    const int g0 = unit * NBOARD;
     bool ovf = false;
     // optional device timestamps (bench.py: the launch's span inside a replayed HIP graph):
     // s_memrealtime (100 MHz) at the workgroup's start and end
@@ -544,7 +559,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     // a compacted leaf batch (rvz_search_compact): dead boards are not evaluated, their rows are
     // never read (uniform exit before the first barrier; NBOARD divides the stripe)
     static_assert(RVZ_LIVE_STRIPE % NBOARD == 0, "stripe granule");
-    if (row_dead(n_live, g0)) {
+    if (g0 >= n_boards || row_dead(n_live, g0)) {
         if (stamps && tid == 0) {
             stamps[0] = t_start;
             stamps[1] = __builtin_amdgcn_s_memrealtime();
@@ -687,9 +702,23 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
 }  // namespace
 
 // workgroups of one h2 trunk launch (k_resnet_h2's grid)
-static int h2_grid(int bs, int filters, int n) {
+// RVZ_H2_DYN 1 (default): board units dealt to workgroups in start order (k_resnet_h2, `claim`).
+// Under this load the eight XCDs hold different clocks (1.73-1.92 GHz, power-limited at ~1.3 kW;
+// profiles/r02ac_power.txt), and blocks are dealt round-robin over the XCDs, so with one unit per
+// block the slowest XCD set the pace and the faster ones idled at the end of every launch. With
+// 1/8 spare workgroups the faster XCDs take more units: C2 +2.2%, C3 +2.5%, C5 +2.2%
+// (whole-bench A/Bs, profiles/r02ad_ab_dyn.txt).
+#ifndef RVZ_H2_DYN
+#define RVZ_H2_DYN 1
+#endif
+// board units of one h2 trunk launch, and its grid (RVZ_H2_DYN: + 1/8 spare workgroups, at least 8)
+static int h2_units(int bs, int filters, int n) {
     if (bs == 6) return filters == 64 ? (n + 3) / 4 : n;
     return filters == 64 ? (n + 1) / 2 : n;
+}
+static int h2_grid(int bs, int filters, int n) {
+    const int u = h2_units(bs, filters, n);
+    return RVZ_H2_DYN && u > 0 ? u + ((u + 63) / 64) * 8 : u;
 }
 
 template <int BS>
@@ -698,22 +727,28 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
                             const int32_t* n_live, uint64_t* stamps, const uint32_t* stamp_ctr,
                             int ring) {
     const Layout L = make_layout(filters, blocks, BS);
+    const dim3 grid(h2_grid(BS, filters, n));
+    // the unit counter: word n*192 + 1 of the (zero-initialised) workspace
+    uint32_t* claim = RVZ_H2_DYN ? reinterpret_cast<uint32_t*>(work + (size_t)n * 192 + 1) : nullptr;
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
 #endif
     if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
         if (filters == 64)
-            hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), dim3((n + 3) / 4), dim3(256), 0, s,
-                               x, n, params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
+            hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), grid, dim3(256), 0, s, x, n,
+                               params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
+                               claim);
         else
-            hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), dim3(n), dim3(256), 0, s, x, n,
-                               params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
+            hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 3, 6, 2>), grid, dim3(256), 0, s, x, n,
+                               params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
+                               claim);
     } else if (filters == 64)
-        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), dim3((n + 1) / 2), dim3(256),
-                           RVZ_H2_DYN_LDS, s, x, n, params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
+        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), grid, dim3(256), RVZ_H2_DYN_LDS, s, x,
+                           n, params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
+                           claim);
     else
-        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), dim3(n), dim3(256), 0, s, x, n,
-                           params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring);
+        hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), grid, dim3(256), 0, s, x, n, params,
+                           L, blob, blocks, work, n_live, stamps, stamp_ctr, ring, claim);
 }
 
 extern "C" {
@@ -746,7 +781,8 @@ int rvz_phase_read(uint64_t* host, int n) {
                    hipSuccess ? 0 : -5;
 }
 #endif
-// + 4 floats: word n*192 is the h2 kernel's sticky activation-overflow flag
+// + 4 floats: word n*192 is the h2 kernel's sticky activation-overflow flag, word n*192 + 1 its
+// unit counter (RVZ_H2_DYN); both must be zero before the first launch on a workspace
 int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192 + 4; }
 int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const float* params,
                            int32_t filters, int32_t blocks, float* logits, float* value,
