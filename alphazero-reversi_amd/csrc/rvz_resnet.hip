@@ -711,14 +711,17 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
 #ifndef RVZ_H2_DYN
 #define RVZ_H2_DYN 1
 #endif
-// board units of one h2 trunk launch, and its grid (RVZ_H2_DYN: + 1/8 spare workgroups, at least 8)
+#ifndef RVZ_H2_SPARE
+#define RVZ_H2_SPARE 8        // 1/RVZ_H2_SPARE spare workgroups (a multiple of 8, at least 8)
+#endif
+// board units of one h2 trunk launch, and its grid (RVZ_H2_DYN: + 1/RVZ_H2_SPARE spare workgroups)
 static int h2_units(int bs, int filters, int n) {
     if (bs == 6) return filters == 64 ? (n + 3) / 4 : n;
     return filters == 64 ? (n + 1) / 2 : n;
 }
 static int h2_grid(int bs, int filters, int n) {
     const int u = h2_units(bs, filters, n);
-    return RVZ_H2_DYN && u > 0 ? u + ((u + 63) / 64) * 8 : u;
+    return RVZ_H2_DYN && u > 0 ? u + ((u + 8 * RVZ_H2_SPARE - 1) / (8 * RVZ_H2_SPARE)) * 8 : u;
 }
 
 template <int BS>
