@@ -195,11 +195,11 @@ struct H2W {
     }
 };
 // f16x8 index of k-step `it` of a layer (it >= NIT: the next layer's) from the layer's base:
-// [tap][kstep][part][ctile][lane]. mirror (ILV pixel group 1): the wave walks the tap rows in
-// reverse, so both groups meet their edge taps at the same it.
+// [tap][kstep][part][ctile][lane]. mirror (ILV pixel group 1, RVZ_H2_MIRROR 1 or 2): the wave
+// walks the tap rows in reverse, so both groups meet their edge taps at the same it.
 #ifndef RVZ_H2_MIRROR
-#define RVZ_H2_MIRROR 2      // 1: (dr, dc) -> (-dr, -dc); 2: rows only, (dr, dc) -> (-dr, dc)
-#endif
+#define RVZ_H2_MIRROR 0      // 0: natural order, a skip window per pixel group (conv_h2);
+#endif                       // 1: (dr, dc) -> (-dr, -dc); 2: rows only, (dr, dc) -> (-dr, dc)
 // the natural tap a mirrored wave reads at iteration tap t
 __host__ __device__ constexpr int h2_mirror_tap(int t) {
     return RVZ_H2_MIRROR == 1 ? 8 - t : (2 - t / 3) * 3 + t % 3;
@@ -380,7 +380,7 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
         out, acc, er, wt, lane, ovf);
 }
 
-template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV>
+template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                         const H2W& wr, int wl,   // layer base, f16x8 units
                                         const float* __restrict__ bias,
@@ -391,16 +391,28 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     using C = CfgH<F, G::NPIX>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
     // ILV: tile 0 is board row 0 (pixel group 0) or row 7 (group 1), and the taps with dr = -1
-    // (row 0) or dr = +1 (row 7) leave the boards for all its pixels. Group 1 walks the tap rows
-    // in reverse (dr -> -dr, RVZ_H2_MIRROR 2), so both groups skip tile 0's A loads and MFMAs in
-    // k-steps [0, SKIP), a compile-time window, and still fetch the same weight fragments
-    // together in the middle row (dr = 0). Measured (tools/ab_h2.py, one box, C2 trunk): -3.2%
-    // against no skip (profiles/r02k_ab_h2_mirror_c2.json); the full mirror (dr, dc -> -dr, -dc)
-    // shares only the centre tap: -2.1%. Instantiating the k-loop once per group instead (both
-    // in natural order) spilled 74 VGPRs.
-    constexpr int SKIP = ILV ? 3 * KS : 0;
+    // (row 0) or dr = +1 (row 7) leave the boards for all its pixels: tile 0's A loads and MFMAs
+    // are skipped in those k-steps (1/12 of the conv MFMAs).
+    // RVZ_H2_MIRROR 0 (default, NAT): both groups walk the taps in natural order, so the two waves
+    // of a channel group fetch the same weight fragments at about the same time (L1 hits), and
+    // each skips in its own window, group 0 in [0, 3 KS) (dr = -1), group 1 in [6 KS, 9 KS)
+    // (dr = +1), both compile-time: the kernel instantiates the whole trunk once per group (GRP)
+    // behind one wave-uniform branch (190 VGPRs; the same choice made per layer needed 224, per
+    // k-step 248). Whole-bench A/B, one box: +2.8% over the row mirror
+    // (profiles/r02ah_ab_nat.txt).
+    // RVZ_H2_MIRROR 2 (row mirror): group 1 walks the tap rows in reverse (dr -> -dr) so both
+    // groups skip in k-steps [0, 3 KS) and share fragments only in the middle tap row: -3.2%
+    // trunk against no skip (profiles/r02k_ab_h2_mirror_c2.json); 1 (full mirror) shares only
+    // the centre tap: -2.1%.
+    constexpr bool NAT = ILV && RVZ_H2_MIRROR == 0;
     const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
-    const bool mirror = ILV && wave / WaveTilesH<F, CTW, PTW>::CG != 0;
+    const bool mirror = ILV && !NAT && wave / WaveTilesH<F, CTW, PTW>::CG != 0;
+    // is tile 0 skipped in k-step i (compile-time once the k-loop is unrolled)
+    auto skip0 = [](int i) -> bool {
+        if (!ILV) return false;
+        if (NAT) return GRP == 0 ? i < 3 * KS : (i >= 6 * KS && i < 9 * KS);
+        return i < 3 * KS;
+    };
     load_epi(er, bias, isc, wt, lane);                // lands during the k-loop
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
     unsigned pmask[PTW];                              // valid taps in iteration order
@@ -428,7 +440,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         const int t = it / KS, ks = it - t * KS;
         const int off = mirror ? G::tap_offset(h2_mirror_tap(t)) : G::tap_offset(t);
 #pragma unroll
-        for (int u = (it < SKIP ? 1 : 0); u < PTW; ++u) {
+        for (int u = (skip0(it) ? 1 : 0); u < PTW; ++u) {
             const int nat = wt.px[u] + off;
             const int row = (pmask[u] >> t) & 1u ? nat : C::ZROW + (nat & 7);
             const uint16_t* ap = in + C::at(row, 0, kq) + ks * C::KSP;
@@ -452,13 +464,15 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         const int ia = it + APD;                      // the A operands loaded this k-step
         if (ia < NIT) load_a(aq[ia % (APD + 1)], ia);
         load_b(bq[it + PD], it + PD);
-        if (it < SKIP) {
+        const bool sa = ia < NIT && skip0(ia);        // next A load without tile 0
+        if (skip0(it)) {
             mma3<CTW, PTW, 1>(acc, aq[it % (APD + 1)], bq[it]);
-            if (ia < SKIP) interleave_loads<0, 3 * CTW * (PTW - 1), 2 * (PTW - 1), 2 * CTW>();
+            if (sa) interleave_loads<0, 3 * CTW * (PTW - 1), 2 * (PTW - 1), 2 * CTW>();
             else interleave_loads<0, 3 * CTW * (PTW - 1), 2 * PTW, 2 * CTW>();
         } else {
             mma3(acc, aq[it % (APD + 1)], bq[it]);
-            interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+            if (sa) interleave_loads<0, 3 * CTW * PTW, 2 * (PTW - 1), 2 * CTW>();
+            else interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -578,48 +592,58 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     // (issuing the stem's loads before the first conv's weight prefetch measured neutral: the
     // stem's epilogue time is the partner workgroup's MFMAs sharing the SIMD, not a load wait)
     const H2W wr(blob, h2_blob_elems(F, n_blocks));
-    f16x8 bc[RVZ_H2_PD][CTW][2];
-    if (n_blocks > 0) {
-        const int wu = WT(wave, lane).ct0 * 64;
-        const bool mirror = ILV && wave / WT::CG != 0;
+    // from the weight prefetch to the last residual block; NAT (RVZ_H2_MIRROR 0): one instance
+    // per pixel group (its own tile-0 skip window), chosen by a wave-uniform branch
+    const bool grp1 = ILV && RVZ_H2_MIRROR == 0 && wave / WT::CG != 0;
+    auto trunk = [&](auto grp) {
+        constexpr int GR = decltype(grp)::value;
+        f16x8 bc[RVZ_H2_PD][CTW][2];
+        if (n_blocks > 0) {
+            const int wu = WT(wave, lane).ct0 * 64;
+            const bool mirror = ILV && RVZ_H2_MIRROR != 0 && wave / WT::CG != 0;   // as conv_h2
 #pragma unroll
-        for (int s = 0; s < RVZ_H2_PD; ++s) {
-            const int f = wu + h2_frag<F>(s, mirror);
+            for (int s = 0; s < RVZ_H2_PD; ++s) {
+                const int f = wu + h2_frag<F>(s, mirror);
 #pragma unroll
-            for (int c = 0; c < CTW; ++c)
+                for (int c = 0; c < CTW; ++c)
 #pragma unroll
-                for (int p = 0; p < 2; ++p) bc[s][c][p] = wr.load(f + (p * C::CT + c) * 64, lane);
+                    for (int p = 0; p < 2; ++p) bc[s][c][p] = wr.load(f + (p * C::CT + c) * 64, lane);
+            }
         }
-    }
-    XinStage<NBOARD, BS, NTHR> st;
-    st.load(x, n_boards, g0, tid);
-    EpiH<CTW, PTW> er;
-    f16x8 ws[CTW][2];
-    stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
-    STEM_T(0);
-    st.store(xin, tid);
-    STEM_T(1);
-    __syncthreads();
-    STEM_T(2);
-    stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
-    STEM_T(3);
-    __syncthreads();
-    PHASE(1);
-    const int64_t LW = h2_layer_elems(F);
-    const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
-    for (int blk = 0; blk < n_blocks; ++blk) {
-        const int l1 = 2 * blk, l2 = 2 * blk + 1;
-        conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV>(actA, actB, wr, (int)(l1 * LW / 8),
-                                                prm + L.res_b + (size_t)l1 * F, isc + l1 * F,
-                                                wave, lane, bc, er, ovf);
-        if (blk == 0) PHASE(5);
+        XinStage<NBOARD, BS, NTHR> st;
+        st.load(x, n_boards, g0, tid);
+        EpiH<CTW, PTW> er;
+        f16x8 ws[CTW][2];
+        stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+        STEM_T(0);
+        st.store(xin, tid);
+        STEM_T(1);
         __syncthreads();
-        if (blk == 0) PHASE(6);
-        conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV>(actB, actA, wr, (int)(l2 * LW / 8),
-                                               prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
-                                               wave, lane, bc, er, ovf);
+        STEM_T(2);
+        stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
+        STEM_T(3);
         __syncthreads();
-    }
+        PHASE(1);
+        const int64_t LW = h2_layer_elems(F);
+        const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
+        for (int blk = 0; blk < n_blocks; ++blk) {
+            const int l1 = 2 * blk, l2 = 2 * blk + 1;
+            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
+                                                          prm + L.res_b + (size_t)l1 * F,
+                                                          isc + l1 * F, wave, lane, bc, er, ovf);
+            if (blk == 0) PHASE(5);
+            __syncthreads();
+            if (blk == 0) PHASE(6);
+            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR>(actB, actA, wr, (int)(l2 * LW / 8),
+                                                         prm + L.res_b + (size_t)l2 * F,
+                                                         isc + l2 * F, wave, lane, bc, er, ovf);
+            __syncthreads();
+        }
+    };
+    if (grp1)
+        trunk(std::integral_constant<int, 1>{});
+    else
+        trunk(std::integral_constant<int, 0>{});
     PHASE(2);
     // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
     head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA}, reinterpret_cast<float*>(actB),
