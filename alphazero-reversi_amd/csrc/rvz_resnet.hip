@@ -525,7 +525,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, const int32_t* __restrict__ n_live,
                  uint64_t* __restrict__ stamps, const uint32_t* __restrict__ stamp_ctr,
-                 int ring, uint32_t* __restrict__ claim) {
+                 int ring, unsigned long long* __restrict__ claim) {
     using WT = WaveTilesH<F, CTW, PTW>;
     // row-interleaved pair of 8x8 boards (GeoH ILV): two pixel groups of 4 tiles = 8 board rows
     constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
@@ -548,13 +548,12 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     if (claim) {
         // RVZ_H2_DYN: board units are dealt in workgroup start order from a counter in the
         // workspace, over a grid larger than the units; the workgroups that start last (on the
-        // XCDs that run slowest) find none left and exit. The last of the grid's claims re-arms the
-        // counter for the next launch (stream order), so it is zero at every launch start.
+        // XCDs that run slowest) find none left and exit. The 64-bit counter is never reset: each
+        // launch adds exactly gridDim.x, so claim mod gridDim.x covers every unit once per launch
+        // whatever the counter held below 2^63 (a zeroed workspace keeps the spare units last).
         __shared__ int s_unit;
         if (tid == 0) {
-            const uint32_t u = atomicAdd(claim, 1u);
-            if (u == gridDim.x - 1) atomicExch(claim, 0u);
-            s_unit = (int)u;
+            s_unit = (int)(atomicAdd(claim, 1ull) % gridDim.x);
         }
         __syncthreads();
         unit = s_unit;
@@ -755,8 +754,9 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
                             int ring) {
     const Layout L = make_layout(filters, blocks, BS);
     const dim3 grid(h2_grid(BS, filters, n));
-    // the unit counter: word n*192 + 1 of the (zero-initialised) workspace
-    uint32_t* claim = RVZ_H2_DYN ? reinterpret_cast<uint32_t*>(work + (size_t)n * 192 + 1) : nullptr;
+    // the unit counter: words n*192 + 2, 3 of the workspace (8-byte aligned)
+    unsigned long long* claim =
+        RVZ_H2_DYN ? reinterpret_cast<unsigned long long*>(work + (size_t)n * 192 + 2) : nullptr;
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
 #endif
@@ -808,8 +808,8 @@ int rvz_phase_read(uint64_t* host, int n) {
                    hipSuccess ? 0 : -5;
 }
 #endif
-// + 4 floats: word n*192 is the h2 kernel's sticky activation-overflow flag, word n*192 + 1 its
-// unit counter (RVZ_H2_DYN); both must be zero before the first launch on a workspace
+// + 4 floats: word n*192 is the h2 kernel's sticky activation-overflow flag (zero it before the
+// first launch), words n*192 + 2, 3 its 64-bit unit counter (RVZ_H2_DYN; any value below 2^63)
 int64_t rvz_resnet_work_size(int32_t n) { return n < 0 ? RVZ_EINVAL : (int64_t)n * 192 + 4; }
 int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const float* params,
                            int32_t filters, int32_t blocks, float* logits, float* value,

@@ -194,10 +194,10 @@ int rvz_resnet_heads_fc(int32_t board, const float *work, int32_t n, const float
  * accumulator (error of an fp32 GEMM; see csrc/rvz_resnet.hip k_resnet_h2). Boards 8 and 6.
  * blob: rvz_resnet_h2_weights' output (scaled f16 parts + inverse scales, once per parameter
  * update), rvz_resnet_h2_size(filters, blocks) uint16 elements, 16-byte aligned.
- * work: rvz_resnet_work_size(n) floats, zero-initialised by the caller before its first use;
- * work[n * 192] is set to 1 (never cleared by the kernel) if an activation reached the f16 range
- * limit 65520, i.e. the outputs are not valid; word n * 192 + 1 is the trunk's board-unit
- * counter (units dealt to workgroups in start order; zero again after every launch). */
+ * work: rvz_resnet_work_size(n) floats (16-byte aligned); work[n * 192] (zero it before the first
+ * use) is set to 1 (never cleared by the kernel) if an activation reached the f16 range limit
+ * 65520, i.e. the outputs are not valid; words n * 192 + 2, 3 hold the trunk's 64-bit board-unit
+ * counter (units dealt to workgroups in start order; any initial value below 2^63). */
 int64_t rvz_resnet_h2_size(int32_t filters, int32_t blocks);
 int rvz_resnet_h2_weights(const float *params, int32_t filters, int32_t blocks, uint16_t *blob,
                           void *hip_stream);

@@ -304,3 +304,25 @@ def test_h2_live_rows(board, filters, n, lives):
         assert torch.equal(value[a:a + live], v0[a:a + live]), s
         tail = a + -(-live // 16) * 16
         assert bool(torch.isnan(logits[tail:e]).all()) and bool(torch.isnan(value[tail:e]).all())
+
+
+@pytest.mark.parametrize("board,filters,n", [(8, 64, 300), (6, 64, 97), (8, 128, 37)])
+def test_h2_unit_counter_any_start(board, filters, n):
+    """The trunk deals its board units to workgroups in start order from a 64-bit counter in the
+    workspace (words n*192 + 2, 3; RVZ_H2_DYN), never reset: whatever the counter holds (below
+    2^63), every unit is evaluated exactly once per launch, so the outputs are bit-identical to a fresh
+    workspace's, launch after launch."""
+    import rvz
+    torch.manual_seed(board * filters + n)
+    net = rvz.AlphaZeroNetwork(board, 2, filters).cuda().eval()
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    x = (torch.rand(n, 3, board, board, device="cuda") > 0.6).float()
+    l0, v0 = (t.clone() for t in ev(x))
+    work = ev._outs[n][2]
+    ctr = work[n * 192 + 2:n * 192 + 4].view(torch.int64)
+    for start in (1, 12345678901, 2 ** 62 + 7):
+        ctr.fill_(start)
+        for _ in range(3):
+            lg, vl = ev(x)
+            assert torch.equal(lg, l0) and torch.equal(vl, v0), start
+    assert not ev.overflowed()
