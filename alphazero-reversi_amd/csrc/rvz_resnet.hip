@@ -519,6 +519,10 @@ struct XinStage {
 #else
 #define RVZ_H2_VGPR_ATTR
 #endif
+// bits 52-55 of a workgroup's end stamp: the XCD it ran on (HW_REG_XCC_ID; bench.py --stamps-dump)
+__device__ __forceinline__ uint64_t stamp_xcc() {
+    return (uint64_t)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xF) << 52;
+}
 template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) RVZ_H2_VGPR_ATTR
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
@@ -575,7 +579,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     if (g0 >= n_boards || row_dead(n_live, g0)) {
         if (stamps && tid == 0) {
             stamps[0] = t_start;
-            stamps[1] = __builtin_amdgcn_s_memrealtime();
+            stamps[1] = __builtin_amdgcn_s_memrealtime() | stamp_xcc();
         }
         return;
     }
@@ -658,7 +662,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         __syncthreads();
         if (tid == 0) {
             stamps[0] = t_start;
-            stamps[1] = __builtin_amdgcn_s_memrealtime() | (nb << 56);
+            stamps[1] = __builtin_amdgcn_s_memrealtime() | stamp_xcc() | (nb << 56);
         }
     }
 }

@@ -11,7 +11,7 @@ from typing import Optional
 import torch
 
 TICKS_PER_MS = 1e5          # s_memrealtime: 100 MHz
-_END_MASK = (1 << 56) - 1
+_END_MASK = (1 << 52) - 1      # bits 52-55: XCD id, 56-63: evaluated boards
 
 
 def trunk_spans(stamps: torch.Tensor, launches: int) -> Optional[dict]:

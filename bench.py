@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--joined-lanes", action="store_true",
                     help="one graph for all lanes with a fork / join per ply (default: one "
                          "graph per lane on its own stream, no per-ply join; +0.9%% at C2)")
+    ap.add_argument("--stamps-dump", default=None,
+                    help="save lane 0's trunk stamp ring of the timed region (int64 [launch, "
+                         "workgroup, 2]; tools/xcd_balance.py) to this .npy path")
     ap.add_argument("--no-stamps", action="store_true",
                     help="no device stamps in the timed graph (roofline from the isolated "
                          "back-to-back launches)")
@@ -543,6 +546,9 @@ def main():
     if graph_events:
         from rvz.measure import trunk_spans
         trunk_live = trunk_spans(graph_events[0], int(graph_events[1].item()))
+        if args.stamps_dump and rank == 0:
+            n_st = min(int(graph_events[1].item()), graph_events[0].shape[0])
+            np.save(args.stamps_dump, graph_events[0][:n_st].cpu().numpy())
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)

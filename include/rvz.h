@@ -214,7 +214,8 @@ int rvz_resnet_trunk_h2(int32_t board, const float *x, int32_t n, const float *p
  * depend on the row's position in the batch (tests/test_gpu_network.py). stamps (nullable,
  * bench.py): every trunk workgroup w stores the device's 100 MHz wall clock (s_memrealtime) at its
  * start and end in stamps[2w], stamps[2w+1] (uint64 [rvz_resnet_h2_grid(board, filters, n)][2];
- * bits 56-63 of the end stamp: the workgroup's evaluated boards, 0 for a dead workgroup):
+ * bits 56-63 of the end stamp: the workgroup's evaluated boards, 0 for a dead workgroup; bits
+ * 52-55: the XCD it ran on):
  * max(end) - min(start) is the launch's span, readable after a replayed HIP graph (torch's HIP
  * runtime refuses external event records in stream capture). stamp_ctr (device uint32, nullable):
  * stamps is a ring of `ring` such launch rows and the trunk writes row *stamp_ctr % ring; the

@@ -259,7 +259,8 @@ def test_h2_timing_forms_are_bit_identical():
     assert torch.equal(l0, l1) and torch.equal(v0, v1)
     assert torch.equal(l0, l2) and torch.equal(v0, v2)
     s = stamps[0].cpu()
-    end = s[:, 1] & ((1 << 56) - 1)
+    end = s[:, 1] & ((1 << 52) - 1)
+    assert bool((((s[:, 1] >> 52) & 0xF) < 8).all())      # the XCD id field
     assert bool((s > 0).all()) and bool((end >= s[:, 0]).all())
     assert int((s[:, 1] >> 56).sum()) == 96          # evaluated boards, per workgroup
     assert bool((stamps[1] == 0).all())

@@ -46,13 +46,17 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
                                       C.c_void_p(_lib.stream_handle()))
         assert rc == 0
     torch.cuda.synchronize()
-    nwg = (n + 1) // 2 if filters == 64 else n
-    buf = np.zeros((nwg, 8), np.uint64)
-    assert lib.rvz_phase_read(buf.ctypes.data_as(C.c_void_p), nwg) == 0
-    b = buf.astype(np.int64)
-    wv = np.zeros((nwg, 16), np.uint64)
-    assert lib.rvz_wave_read(wv.ctypes.data_as(C.c_void_p), nwg) == 0
-    wv = wv.astype(np.int64)
+    # records are per workgroup (blockIdx); with dealt units (RVZ_H2_DYN) the grid has spare
+    # workgroups that find no unit and record nothing: keep the workgroups that ran a unit
+    ngrid = lib.rvz_resnet_h2_grid(8, filters, n)
+    buf = np.zeros((ngrid, 8), np.uint64)
+    assert lib.rvz_phase_read(buf.ctypes.data_as(C.c_void_p), ngrid) == 0
+    ran = buf[:, 3] != 0
+    b = buf.astype(np.int64)[ran]
+    wv = np.zeros((ngrid, 16), np.uint64)
+    assert lib.rvz_wave_read(wv.ctypes.data_as(C.c_void_p), ngrid) == 0
+    wv = wv.astype(np.int64)[ran]
+    nwg = int(ran.sum())
     d = np.diff(b[:, :4], axis=1)
     tot = b[:, 3] - b[:, 0]
     key = f"{blocks}x{filters}"
@@ -63,9 +67,9 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
                 "l0_barrier": float((b[:, 6] - b[:, 5]).mean()),
                 "n_wg": nwg}
     if hasattr(lib, "rvz_stem_read"):    # builds with the stem stamps (STEM_T)
-        st = np.zeros((nwg, 8), np.uint64)
-        assert lib.rvz_stem_read(st.ctypes.data_as(C.c_void_p), nwg) == 0
-        st = st.astype(np.int64)
+        st = np.zeros((ngrid, 8), np.uint64)
+        assert lib.rvz_stem_read(st.ctypes.data_as(C.c_void_p), ngrid) == 0
+        st = st.astype(np.int64)[ran]
         out[key]["stem_split"] = {"zero_rows_issue_loads": float((st[:, 0] - b[:, 0]).mean()),
                                   "xin_store_wait_loads": float((st[:, 1] - st[:, 0]).mean()),
                                   "sync1": float((st[:, 2] - st[:, 1]).mean()),
@@ -74,9 +78,9 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
                                   "mfma": float((st[:, 5] - st[:, 4]).mean()),
                                   "epilogue": float((st[:, 3] - st[:, 5]).mean()),
                                   "sync2": float((b[:, 1] - st[:, 3]).mean())}
-    rt = np.zeros((nwg, 2), np.uint64)
-    assert lib.rvz_rt_read(rt.ctypes.data_as(C.c_void_p), nwg) == 0
-    rt = rt.astype(np.int64)
+    rt = np.zeros((ngrid, 2), np.uint64)
+    assert lib.rvz_rt_read(rt.ctypes.data_as(C.c_void_p), ngrid) == 0
+    rt = rt.astype(np.int64)[ran]
     wg_us = (rt[:, 1] - rt[:, 0]) / 100.0                    # 100 MHz
     out[key]["wg_us_mean"] = float(wg_us.mean())
     out[key]["clock_ghz"] = float(tot.mean() / wg_us.mean() / 1e3)
@@ -89,8 +93,9 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
     out[key]["end_us_pct"] = [round(float(np.percentile(en, q)), 2) for q in (0, 10, 25, 50, 75, 90, 100)]
     out[key]["wg_us_pct"] = [round(float(np.percentile(wg_us, q)), 2) for q in (0, 10, 50, 90, 100)]
     if hasattr(lib, "rvz_hwid_read") and kern == "h2":
-        hw = np.zeros((nwg, 2), np.uint32)
-        assert lib.rvz_hwid_read(hw.ctypes.data_as(C.c_void_p), nwg) == 0
+        hw = np.zeros((ngrid, 2), np.uint32)
+        assert lib.rvz_hwid_read(hw.ctypes.data_as(C.c_void_p), ngrid) == 0
+        hw = hw[ran]
         # CU identity: XCC, SE (bits 13-15), SH (12), CU (8-11)
         cu = (hw[:, 1].astype(np.int64) & 0xF) * 4096 + ((hw[:, 0] >> 8) & 0xFF).astype(np.int64)
         by = {}
@@ -109,6 +114,10 @@ for blocks, filters, n in ((6, 64, 4096), (10, 128, 4096)):
                         if len(first_pair) < 8:
                             first_pair.append([w, v])
         d = np.array(dstart) if dstart else np.zeros(1)
+        xcc = hw[:, 1].astype(np.int64) & 0xF
+        out[key]["units_per_xcc"] = [int((xcc == k).sum()) for k in range(8)]
+        out[key]["wg_us_per_xcc"] = [round(float(wg_us[xcc == k].mean()), 2) if (xcc == k).any()
+                                     else None for k in range(8)]
         out[key]["cus_used"] = len(by)
         out[key]["wg_per_cu"] = [min(len(v) for v in by.values()), max(len(v) for v in by.values())]
         out[key]["coresident_pairs"] = pairs
