@@ -549,8 +549,14 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
 // One search round: the previous batch's expand + backup (when a submit is pending), then the
 // next batch's selection, in one launch (one wave per game). Every load that does not depend on
 // another is issued at the head.
+// RVZ_STEP_WPE (experiments): amdgpu_waves_per_eu cap of k_step (e.g. 7 = 72 VGPRs)
+#ifdef RVZ_STEP_WPE
+#define RVZ_STEP_ATTR __attribute__((amdgpu_waves_per_eu(RVZ_STEP_WPE)))
+#else
+#define RVZ_STEP_ATTR
+#endif
 template <int BS, typename XT>
-__global__ __launch_bounds__(256) void k_step(View v, int expand, const float* __restrict__ policy,
+__global__ __launch_bounds__(256) RVZ_STEP_ATTR void k_step(View v, int expand, const float* __restrict__ policy,
                                               int is_logits, const float* __restrict__ value,
                                               int first, int bsz, int eb,
                                               XT* __restrict__ leaf_x,

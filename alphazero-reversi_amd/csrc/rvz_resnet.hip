@@ -212,15 +212,16 @@ __device__ __forceinline__ int h2_frag(int it, bool mirror) {
     return (lay * NIT + tn * KS + ks) * KSTEP;
 }
 
-// RVZ_H2_SKIP_LDS 1 (default): the skip input is re-read from LDS as its two parts (x0 + x1,
-// 22 bits: the precision the conv inputs already carry; no measurable error change,
-// tools/emu_split.py f16x2_1acc_lds) at the place conv B overwrites it, instead of kept in 32
-// fp32 registers. The trunk then needs 216 VGPRs instead of 248, so a k_step or k_act wave (80)
-// fits on a SIMD beside the two trunk waves (2 x 216 + 80 = 512) instead of taking a trunk
-// workgroup's place: the kernel alone is ~1.4% slower, the whole C2 ply 0.9% faster (one-box
-// bench A/B, profiles/r02s_ablib_skiplds.txt).
+// RVZ_H2_SKIP_LDS 1: the skip input is re-read from LDS as its two parts (x0 + x1, 22 bits: the
+// precision the conv inputs already carry; tools/emu_split.py f16x2_1acc_lds) at the place conv B
+// overwrites it, instead of kept in 32 fp32 registers. With the mirrored tap order (216 vs 248
+// VGPRs) that let a k_step or FC-heads wave (<= 80) share a SIMD with the two trunk waves:
+// +0.9-1.6% per ply (profiles/r02s_ablib_skiplds.txt, r02u). Under the natural-order trunk
+// (190 vs 220 VGPRs) the registers win: 0 (default) is +1.05% per ply
+// (profiles/r02ap_ab_skipreg.txt); `k_act` (63) still fits beside two 220-VGPR waves, k_step and
+// the heads capped at 72 measured the same (profiles/r02aq_ab_caps.txt).
 #ifndef RVZ_H2_SKIP_LDS
-#define RVZ_H2_SKIP_LDS 1
+#define RVZ_H2_SKIP_LDS 0
 #endif
 template <int CTW, int PTW>
 struct EpiH {

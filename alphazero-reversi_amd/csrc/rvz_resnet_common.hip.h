@@ -139,8 +139,11 @@ __device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int
 #ifndef RVZ_HEADS_PD
 #define RVZ_HEADS_PD 4
 #endif
+#ifndef RVZ_HEADS_WPE
+#define RVZ_HEADS_WPE 6      // waves per SIMD the heads are built for (6: <= 80 VGPRs)
+#endif
 #if RVZ_HEADS_STREAM
-#define RVZ_HEADS_ATTR __attribute__((amdgpu_waves_per_eu(6)))
+#define RVZ_HEADS_ATTR __attribute__((amdgpu_waves_per_eu(RVZ_HEADS_WPE)))
 #else
 #define RVZ_HEADS_ATTR
 #endif
