@@ -136,13 +136,15 @@ class SelfPlayRunner:
 
 
 class LaneRunner:
-    """``lanes`` independent SelfPlayRunners ("lanes") of n_games / lanes games each, one stream
-    per lane, captured into ONE HIP graph with a fork / join. The lanes share nothing, so while
-    one lane runs its FC heads, k_step or the tail of its trunk kernel, the other lanes' trunk
-    workgroups fill the CUs (tools/exp_lanes.py: two 2048-board evaluator chains in one graph
-    take 0.443 ms per call against 0.458 for one 4096-board chain).
-    Game g of lane l is global game l * (n_games / lanes) + g with the same seed as in one
-    runner of n_games: the games, trees and moves are those of the single-lane run.
+    """``lanes`` independent SelfPlayRunners ("lanes"), one stream per lane, captured into ONE HIP
+    graph with a fork / join (or one graph per lane, capture(free_run=True)). The lanes share
+    nothing, so while one lane runs its FC heads, k_step or the tail of its trunk kernel, the
+    other lanes' trunk workgroups fill the CUs (tools/exp_lanes.py: two 2048-board evaluator
+    chains in one graph take 0.443 ms per call against 0.458 for one 4096-board chain).
+    The games are split in order into lanes whose sizes differ by at most one (the first
+    n_games % lanes lanes hold one more); game g of a lane starting at global game o is global
+    game o + g with the same seed as in one runner of n_games: the games, trees and moves are
+    those of the single-lane run.
 
     make_engine(n) -> Engine, make_evaluator() -> a callable owning its own output buffers."""
 
@@ -150,14 +152,15 @@ class LaneRunner:
                  n_games: int, lanes: int = 2, temperature: float = 1.0,
                  fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
                  seed_stride: int = None, skip_last_eval: bool = False):
-        if lanes < 1 or n_games % lanes:
-            raise ValueError("n_games must be a multiple of lanes")
-        gl = n_games // lanes
+        if lanes < 1 or n_games < lanes:
+            raise ValueError("need 1 <= lanes <= n_games")
+        sizes = [n_games // lanes + (1 if k < n_games % lanes else 0) for k in range(lanes)]
+        offsets = [sum(sizes[:k]) for k in range(lanes)]
         stride = n_games if seed_stride is None else int(seed_stride)
         self.runners = [SelfPlayRunner(make_engine(gl), make_evaluator(), temperature,
-                                       fused_softmax, autoreset, seed_base + k * gl,
+                                       fused_softmax, autoreset, seed_base + o,
                                        seed_stride=stride, skip_last_eval=skip_last_eval)
-                        for k in range(lanes)]
+                        for gl, o in zip(sizes, offsets)]
         dev = self.runners[0].eng.device
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)]
         self.temperature = float(temperature)

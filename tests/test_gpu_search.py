@@ -339,10 +339,12 @@ def test_skip_last_eval_bit_exact(board, sims):
             assert torch.equal(u, v), k
 
 
-def test_lanes_play_the_same_games():
-    """rvz.LaneRunner (two independent lanes on forked streams, captured into one HIP graph)
-    plays exactly the games of one SelfPlayRunner over the same global game indices: moves,
-    policy vectors and boards bit-identical ply by ply, autoreset included."""
+@pytest.mark.parametrize("n_lanes", [2, 3])
+def test_lanes_play_the_same_games(n_lanes):
+    """rvz.LaneRunner (independent lanes on forked streams, captured into one HIP graph; 3 lanes
+    of 86 / 85 / 85 games) plays exactly the games of one SelfPlayRunner over the same global
+    game indices: moves, policy vectors and boards bit-identical ply by ply, autoreset
+    included."""
     import rvz
     G, plies, sims = 256, 64, 200
     torch.manual_seed(0)
@@ -352,8 +354,8 @@ def test_lanes_play_the_same_games():
         return rvz.Engine(n, num_simulations=sims, batch_size=64)
 
     one = rvz.SelfPlayRunner(make_eng(G), rvz.LeafEvaluator(net), autoreset=True, seed_base=11)
-    two = rvz.LaneRunner(make_eng, lambda: rvz.LeafEvaluator(net), G, lanes=2, autoreset=True,
-                         seed_base=11)
+    two = rvz.LaneRunner(make_eng, lambda: rvz.LeafEvaluator(net), G, lanes=n_lanes,
+                         autoreset=True, seed_base=11)
     one.start()
     two.start()
     for k in range(plies):
@@ -361,11 +363,11 @@ def test_lanes_play_the_same_games():
             r.ply()
             if k == 0:
                 r.capture()         # first ply eager, the rest replayed from the graph
-        la, lb = two.runners
-        assert torch.equal(one.eng.idx_buf, torch.cat([la.eng.idx_buf, lb.eng.idx_buf])), k
-        assert torch.equal(one.eng.p_buf, torch.cat([la.eng.p_buf, lb.eng.p_buf])), k
+        rs = two.runners
+        assert torch.equal(one.eng.idx_buf, torch.cat([r.eng.idx_buf for r in rs])), k
+        assert torch.equal(one.eng.p_buf, torch.cat([r.eng.p_buf for r in rs])), k
         b1 = one.eng.get_state()[0].clone()
-        b2 = torch.cat([la.eng.get_state()[0], lb.eng.get_state()[0]])
+        b2 = torch.cat([r.eng.get_state()[0] for r in rs])
         assert torch.equal(b1, b2), k
     assert int(one.steps.item()) == int(two.steps.item())
     assert int(one.games_done.item()) == int(two.games_done.item()) > 0
@@ -514,8 +516,8 @@ def test_compact_api_errors():
 
 
 def test_bench_configuration_at_full_size_plays_the_plain_games():
-    """The bench's C2 configuration at full size (4,096 games x 800 sims, 6x64 net; 2 free-running
-    lane graphs, compacted leaf batches) against the plain path (one runner, every row
+    """The bench's C2 configuration at full size (4,096 games x 800 sims, 6x64 net; 3 free-running
+    lane graphs of 1,366 / 1,365 / 1,365 games, compacted leaf batches) against the plain path (one runner, every row
     evaluated, eager) over a whole game and its restarts: every ply's moves and the final boards,
     statuses and ply counters are identical."""
     import rvz
@@ -523,7 +525,7 @@ def test_bench_configuration_at_full_size_plays_the_plain_games():
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
     lanes = rvz.LaneRunner(lambda n: rvz.Engine(n, S, 64, compact_leaves=True),
-                           lambda: rvz.LeafEvaluator(net), G, 2, autoreset=True, seed_base=42)
+                           lambda: rvz.LeafEvaluator(net), G, 3, autoreset=True, seed_base=42)
     plain = rvz.SelfPlayRunner(rvz.Engine(G, S, 64), rvz.LeafEvaluator(net), autoreset=True,
                                seed_base=42)
     lanes.start()
