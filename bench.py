@@ -41,12 +41,12 @@ PRESETS = {   # BASELINE.json configs
     # c1: the reference's own plumbing case (one game, 100 sims, the ModelConfig default 5x128
     # net; config.py:14-15) on one GPU, with the CPU port on the same single game beside it
     "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1),
-    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=3),
+    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2),
     "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),
     # per GPU, x8; a step = one self-play + training iteration (main_c4)
     "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, steps=1,
                warmup=0),
-    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=3),
+    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2),
 }
 
 
