@@ -289,6 +289,51 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
         }
 }
 
+// RVZ_H2_HEADS_EPI 1: the last conv's epilogue computes the 1x1 head convs (policy 2, value 1
+// output channels) from its fp32 outputs in registers instead of storing them to LDS for
+// head_convs to read back: per lane, partial dot products over its 4 x CTW channels for each of
+// its PTW pixels, reduced over the four lane groups (shuffles) and, through LDS, over the
+// channel-group waves. Needs the skip input in registers (the output buffer holds the partials).
+#ifndef RVZ_H2_HEADS_EPI
+#define RVZ_H2_HEADS_EPI 0
+#endif
+struct HeadPart {          // the 1x1 head-conv weights (pol_w [2][F], val_w [F]) and LDS partials
+    const float* pol;
+    const float* val;
+    float* part;           // [channel group][3][NPIX]
+};
+template <int F, int NPIX, int CTW, int PTW>
+__device__ __forceinline__ void epilogue_heads(const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
+                                               const WaveTilesH<F, CTW, PTW>& wt, int wave,
+                                               int lane, const f32x4 (&hw)[3][CTW],
+                                               float* __restrict__ part, bool& ovf) {
+    constexpr int CG = WaveTilesH<F, CTW, PTW>::CG;
+    float ph[PTW][3];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u) {
+        ph[u][0] = ph[u][1] = ph[u][2] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]) + er.res[c][u][j];
+                x = fmaxf(x, 0.0f);
+                ovf |= x >= 65520.0f;
+#pragma unroll
+                for (int o = 0; o < 3; ++o) ph[u][o] = fmaf(x, hw[o][c][j], ph[u][o]);
+            }
+    }
+#pragma unroll
+    for (int u = 0; u < PTW; ++u)
+#pragma unroll
+        for (int o = 0; o < 3; ++o) {
+            float v = ph[u][o];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            if (lane < 16) part[((wave % CG) * 3 + o) * NPIX + wt.px[u]] = v;
+        }
+}
+
 __device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
@@ -381,13 +426,14 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
         out, acc, er, wt, lane, ovf);
 }
 
-template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0>
+template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0,
+          bool LASTH = false>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                         const H2W& wr, int wl,   // layer base, f16x8 units
                                         const float* __restrict__ bias,
                                         const float* __restrict__ isc, int wave, int lane,
                                         f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
-                                        bool& ovf) {
+                                        bool& ovf, HeadPart hp = HeadPart{}) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     using C = CfgH<F, G::NPIX>;
     constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
@@ -484,7 +530,18 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
 #pragma unroll
             for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
     // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
-    epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
+    if constexpr (LASTH) {
+        f32x4 hw[3][CTW];                             // the head convs' weights (L2, once)
+#pragma unroll
+        for (int c = 0; c < CTW; ++c) {
+            const int n = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
+            hw[0][c] = *reinterpret_cast<const f32x4*>(hp.pol + n);
+            hw[1][c] = *reinterpret_cast<const f32x4*>(hp.pol + F + n);
+            hw[2][c] = *reinterpret_cast<const f32x4*>(hp.val + n);
+        }
+        epilogue_heads<F, G::NPIX, CTW, PTW>(acc, er, wt, wave, lane, hw, hp.part, ovf);
+    } else
+        epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
 }
 
 // the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for
@@ -599,6 +656,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     // from the weight prefetch to the last residual block; NAT (RVZ_H2_MIRROR 0): one instance
     // per pixel group (its own tile-0 skip window), chosen by a wave-uniform branch
     const bool grp1 = ILV && RVZ_H2_MIRROR == 0 && wave / WT::CG != 0;
+    constexpr bool HEPI = RVZ_H2_HEADS_EPI && !RVZ_H2_SKIP_LDS && ILV;   // C2 shape (F = 128 spilled)
     auto trunk = [&](auto grp) {
         constexpr int GR = decltype(grp)::value;
         f16x8 bc[RVZ_H2_PD][CTW][2];
@@ -630,7 +688,7 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         PHASE(1);
         const int64_t LW = h2_layer_elems(F);
         const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
-        for (int blk = 0; blk < n_blocks; ++blk) {
+        for (int blk = 0; blk < n_blocks - (HEPI ? 1 : 0); ++blk) {
             const int l1 = 2 * blk, l2 = 2 * blk + 1;
             conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
                                                           prm + L.res_b + (size_t)l1 * F,
@@ -643,6 +701,18 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
                                                          isc + l2 * F, wave, lane, bc, er, ovf);
             __syncthreads();
         }
+        if (HEPI && n_blocks > 0) {   // the last block: its conv B ends in the head convs
+            const int l1 = 2 * n_blocks - 2, l2 = 2 * n_blocks - 1;
+            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
+                                                          prm + L.res_b + (size_t)l1 * F,
+                                                          isc + l1 * F, wave, lane, bc, er, ovf);
+            __syncthreads();
+            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, true>(
+                actB, actA, wr, (int)(l2 * LW / 8), prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
+                wave, lane, bc, er, ovf,
+                HeadPart{prm + L.pol_w, prm + L.val_w, reinterpret_cast<float*>(actA)});
+            __syncthreads();
+        }
     };
     if (grp1)
         trunk(std::integral_constant<int, 1>{});
@@ -650,8 +720,25 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         trunk(std::integral_constant<int, 0>{});
     PHASE(2);
     // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
-    head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA}, reinterpret_cast<float*>(actB),
-                                          prm, L, HeadsGlobal{work, g0, n_boards}, tid);
+    if (HEPI && n_blocks > 0) {   // the channel-group partials of the last epilogue, + bias, ReLU
+        constexpr int CELLS = BS * BS, CG = WT::CG;
+        const float* part = reinterpret_cast<const float*>(actA);
+        const HeadsGlobal hpv{work, g0, n_boards};
+        for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
+            const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
+            const int b = rem / CELLS, cell = rem % CELLS;
+            const int px = G::row_of(b, cell);
+            float acc = 0.0f;
+#pragma unroll
+            for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * G::NPIX + px];
+            const float bias = c2 < 2 ? prm[L.pol_b + c2] : prm[L.val_b];
+            hpv.store(b, c2 * CELLS + cell, fmaxf(acc + bias, 0.0f));
+        }
+    } else {
+        head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA},
+                                                  reinterpret_cast<float*>(actB), prm, L,
+                                                  HeadsGlobal{work, g0, n_boards}, tid);
+    }
     PHASE(3);
     RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
