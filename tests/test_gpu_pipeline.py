@@ -33,3 +33,49 @@ def test_selfplay_trainer_iterations_use_the_trained_net(tmp_path):
     assert torch.equal(t["policy_targets"], data["policy_targets"])
     assert torch.equal(t["value_targets"], data["value_targets"])
     assert sum(len(g["states"]) for g in games) == data["states"].shape[0]
+
+
+def test_ddp_trainer_over_rccl_world1_equals_plain_training():
+    """DDPTrainer with a torch.distributed process group on the 'nccl' backend (RCCL on ROCm) at
+    world size 1: every step's gradients go through DDP's bucketed RCCL all-reduce, and the
+    trained parameters equal those of the same steps without a process group, to the run-to-run
+    noise of the plain path itself (MIOpen's backward kernels are not bitwise deterministic:
+    the plain path is run twice and its own spread sets the bound, x4)."""
+    import socket
+    import torch.distributed as dist
+    import rvz
+    from rvz.trainer import DDPTrainer
+    torch.manual_seed(3)
+    n = 512
+    data = {"states": (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float(),
+            "policy_targets": torch.softmax(torch.randn(n, 65, device="cuda"), 1),
+            "value_targets": torch.rand(n, device="cuda") * 2 - 1}
+    nets = []
+    for distributed in (False, False, True):
+        torch.manual_seed(0)
+        net = rvz.AlphaZeroNetwork(8, 2, 64).cuda()
+        if distributed:
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                    world_size=1)
+        try:
+            tr = DDPTrainer(net, batch_size=64)
+            assert tr.distributed == distributed
+            for epoch in range(2):
+                out = tr.train_epoch(data, seed=epoch)
+                assert out["steps"] == n // 64
+            torch.cuda.synchronize()
+        finally:
+            if distributed:
+                dist.destroy_process_group()
+        nets.append(net)
+    sd = [m.state_dict() for m in nets]
+    torch.manual_seed(0)
+    init = rvz.AlphaZeroNetwork(8, 2, 64).cuda().state_dict()
+    moved = max((sd[0][k].float() - init[k].float()).abs().max().item() for k in init)
+    noise = max((sd[0][k].float() - sd[1][k].float()).abs().max().item() for k in init)
+    ddp = max((sd[0][k].float() - sd[2][k].float()).abs().max().item() for k in init)
+    assert moved > 1e-3                       # the nets trained
+    assert ddp <= 4 * noise + 1e-6 * moved, (ddp, noise, moved)
