@@ -826,12 +826,15 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
 #ifndef RVZ_H2_DYN
 #define RVZ_H2_DYN 1
 #endif
+#ifndef RVZ_H2_C5NB
+#define RVZ_H2_C5NB 4         // packed 6x6 at F = 64: boards per workgroup (4: 160 rows, 1 per CU;
+#endif                        // 2: 96 rows, two workgroups per CU)
 #ifndef RVZ_H2_SPARE
 #define RVZ_H2_SPARE 8        // 1/RVZ_H2_SPARE spare workgroups (a multiple of 8, at least 8)
 #endif
 // board units of one h2 trunk launch, and its grid (RVZ_H2_DYN: + 1/RVZ_H2_SPARE spare workgroups)
 static int h2_units(int bs, int filters, int n) {
-    if (bs == 6) return filters == 64 ? (n + 3) / 4 : n;
+    if (bs == 6) return filters == 64 ? (n + RVZ_H2_C5NB - 1) / RVZ_H2_C5NB : n;
     return filters == 64 ? (n + 1) / 2 : n;
 }
 static int h2_grid(int bs, int filters, int n) {
@@ -854,7 +857,8 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
 #endif
     if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
         if (filters == 64)
-            hipLaunchKernelGGL((k_resnet_h2<64, 4, 2, 5, 6, 1>), grid, dim3(256), 0, s, x, n,
+            hipLaunchKernelGGL((k_resnet_h2<64, RVZ_H2_C5NB, 2, RVZ_H2_C5NB == 4 ? 5 : 3, 6,
+                                            RVZ_H2_C5NB == 4 ? 1 : 2>), grid, dim3(256), 0, s, x, n,
                                params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
                                claim);
         else
