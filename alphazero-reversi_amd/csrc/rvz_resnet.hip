@@ -914,7 +914,9 @@ int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const fl
     if (!work || !params || !logits || !value || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128))
         return RVZ_EINVAL;
-    if (((uintptr_t)params & 15) != 0) return RVZ_EINVAL;
+    // the heads copy workspace rows as f32x4: a misaligned workspace is an argument error, not
+    // a device fault
+    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)work & 15) != 0) return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     const Layout L = make_layout(filters, blocks, board);
     const dim3 grid((n + 15) / 16), block(256);
@@ -961,7 +963,11 @@ int rvz_resnet_trunk_h2_ex(int32_t board, const float* x, int32_t n, const float
     if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
         (filters != 64 && filters != 128) || (stamp_ctr && (!stamps || ring <= 0)))
         return RVZ_EINVAL;
-    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
+    // work: 16-byte aligned (the 64-bit unit-counter atomic at words n*192 + 2, 3 and the
+    // heads' f32x4 row copies)
+    if (((uintptr_t)params & 15) != 0 || ((uintptr_t)blob & 15) != 0 ||
+        ((uintptr_t)work & 15) != 0)
+        return RVZ_EINVAL;
     if (n == 0) return RVZ_OK;
     hipStream_t s = (hipStream_t)stream;
     if (board == 8)

@@ -9,7 +9,10 @@ counterpart (mcts.py:220-226,446-542 only chunks one batch over local replicas s
 from __future__ import annotations
 
 import os
-from typing import Tuple
+import socket
+import subprocess
+import time
+from typing import List, Tuple
 
 import torch
 import torch.distributed as dist
@@ -36,16 +39,67 @@ def shard_seeds(seed_base: int, n_total: int, rank: int, world: int) -> torch.Te
     return torch.arange(a, b, dtype=torch.int64) + seed_base
 
 
-def init(backend: str = None) -> bool:
-    """Initialise the default process group when launched by torchrun; False when single-rank."""
+def init(backend: str = None, always: bool = False, device=None) -> bool:
+    """Initialise the default process group when launched with several ranks (torchrun or
+    spawn_ranks); with ``always`` also for a single rank (a one-member group, so a bench line's
+    world size comes from the group itself). False when no group was created."""
     _, _, world = env_rank_world()
-    if world <= 1 or dist.is_initialized():
-        return dist.is_initialized()
+    if dist.is_initialized():
+        return True
+    if world <= 1 and not always:
+        return False
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"   # nccl == RCCL on ROCm
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group(backend=backend)
+    if "MASTER_PORT" not in os.environ:
+        if world > 1:
+            raise RuntimeError("MASTER_PORT must be set for a multi-rank group")
+        os.environ["MASTER_PORT"] = str(free_port())
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", str(world))
+    dist.init_process_group(backend=backend,
+                            device_id=device if backend == "nccl" and device is not None
+                            else None)
     return True
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2) -> int:
+    """Run ``cmd`` as ``n`` rank processes on this node (one per GPU): each child gets RANK =
+    LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n and a shared 127.0.0.1 rendezvous, and
+    inherits stdout/stderr. Children are separate processes started with Popen (never an exec of
+    this one), so call this before anything touches the GPU. Returns 0 when every rank exits 0;
+    otherwise the first failure's code (a signal maps to 1) after terminating the other ranks.
+    This is what `bench.py --gpus N` runs when no launcher (torchrun) set WORLD_SIZE."""
+    if n < 1:
+        raise ValueError("need at least one rank")
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc, alive = 0, list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in alive:            # the exact children of this launcher, nothing else
+                    q.terminate()
+        if alive:
+            time.sleep(poll_s)
+    return rc
 
 
 def _device_for_backend():

@@ -162,8 +162,13 @@ class LeafEvaluator:
                              "(A/B alternatives: tools/alt/alt_eval.py AltEvaluator)")
         if not (dev.type == "cuda" and dtype == torch.float32 and net.board_size in (6, 8)
                 and net.num_filters in (64, 128)):
-            raise _lib.RvzError("LeafEvaluator needs fp32, an 8x8 or 6x6 net of 64 or 128 "
-                                "filters and a HIP device (no CPU fallback)")
+            raise _lib.RvzError(
+                "LeafEvaluator needs fp32, an 8x8 or 6x6 net of 64 or 128 filters and a HIP "
+                f"device (got {net.board_size}x{net.board_size}, {net.num_filters} filters, "
+                f"{dtype}, {dev}; no CPU fallback). For another shape hand the caller any "
+                "callable leaf_x -> (logits, value): rvz.SelfPlay(model, args, evaluator=...), "
+                "ELOPlayer(..., evaluator=...), e.g. evaluator=lambda x: model(x) "
+                "(INTEGRATION.md)")
         self.kernel = "h2"
         # bench.py: (int64 [ring, grid, 2] stamp ring, int32 [1] device launch counter) to time
         # every h2 trunk launch from device wall-clock stamps, or None
@@ -269,6 +274,15 @@ class LeafEvaluator:
         if self.board_size == 8 and f == 64:
             conv = conv * 11 // 12
         return 3 * 2 * rows * f * (32 + conv)
+
+    def useful_flops_per_row(self) -> int:
+        """Algorithmic FLOPs (2 x multiply-adds) of what the trunk kernel computes for one board:
+        the 3 -> F stem, the 2N residual 3x3 convs and the 1x1 head convs (F -> 2 + 1), SURVEY
+        §8(d)'s per-evaluation figure (56.8 MFLOP at 6x64 on 8x8). mfma_flops_per_row / this is
+        the executed/useful ratio (3 f16 products per fp32 product, stem K padding, skipped
+        edge taps)."""
+        cells, f = self.board_size ** 2, self.filters
+        return 2 * cells * (f * 27 + self.n_blocks * 2 * f * f * 9 + f * 3)
 
     # __call__ honours n_live: rows past the live count of a compacted leaf batch are skipped
     accepts_live_count = True

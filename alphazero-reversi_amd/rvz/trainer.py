@@ -119,16 +119,19 @@ class DDPTrainer:
         """One pass over the data. local_data=False: `data` is identical on every rank and each
         rank takes every world-th batch of one seeded permutation. local_data=True: every rank
         holds its own data (its own self-play games, rvz.pipeline) and walks its own permutation
-        (seed + rank). Either way each step's global batch is world x batch_size, and every rank
-        runs the same number of steps (the minimum over ranks). Returns the reference's averaged
-        loss dict (pipeline.py:342-366).
+        (seed * world + rank). Either way each step's global batch is world x batch_size, and
+        every rank runs the same number of steps (the minimum over ranks). Returns the
+        reference's averaged loss dict (pipeline.py:342-366), averaged over ranks too.
         Order: the permutation the reference's DataLoader(shuffle=True) draws when handed a
         generator seeded with `seed` (its base-seed draw, then randperm(n)). On one
         process the last partial batch is trained too, as the reference's DataLoader (no
         drop_last) does; across ranks every step is a full world x batch_size batch."""
         rank, world = self.rank_world()
+        ranks = world
         n = data["states"].shape[0]
-        g = torch.Generator().manual_seed(seed + (rank if local_data else 0))
+        # local data: one stream per (seed, rank) pair, seed * world + rank, so rank r at seed s
+        # never repeats rank r + 1's shuffle at seed s - 1 (the pipeline passes seed + iteration)
+        g = torch.Generator().manual_seed(seed * world + rank if local_data else seed)
         # DataLoader(shuffle=True, generator=g) first draws its workers' base seed from g, then
         # the RandomSampler's permutation: the same two draws give the same batches
         torch.empty((), dtype=torch.int64).random_(generator=g)
@@ -153,6 +156,10 @@ class DDPTrainer:
                                      data["value_targets"][idx])
             tot += torch.stack([x.double() for x in losses])
         tot /= max(1, steps)
+        if self.distributed and ranks > 1:   # the job's loss: the mean over ranks
+            t = tot.to(self.device if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(t)
+            tot = t / ranks
         return {"train/loss": float(tot[0]), "train/policy_loss": float(tot[1]),
                 "train/value_loss": float(tot[2]), "train/lr": self.opt.param_groups[0]["lr"],
                 "steps": steps}

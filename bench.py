@@ -7,18 +7,24 @@
 A step is one self-play ply of every game on the GPU (one 800-simulation MCTS search + one move
 per game: SelfPlay.generate_games' loop body, self_play.py:80-101). The N = 1 workload is
 BASELINE.json configs[1]: 4,096 games, 800 sims, batch 64, 6-block/64-filter ResNet (random init,
-torch.manual_seed(0)), fp32 evaluator (the reference's precision). Games that end restart at once
-from the next seed of their slot, so every step is a steady-state ply. Multi-GPU: one process per
-GPU, each with its own 4,096 games (weak scaling), no collective in the data path.
+torch.manual_seed(0)), fp32-class evaluator (the reference's precision). Games that end restart
+at once from the next seed of their slot, so every step is a steady-state ply.
+
+Multi-GPU: one process per GPU, each with its own 4,096 games (weak scaling), no collective in
+the data path. `--gpus N` without a launcher starts the N rank processes itself
+(rvz.dist.spawn_ranks, before anything touches the GPU); under torchrun the ranks come from its
+environment. Either way every rank checks that the process group's world size equals --gpus.
 
 Printed on rank 0: one JSON line with value = committed plies of all ranks / max-over-ranks wall
-time, the roofline of the dominant rvz kernel (algorithmic bytes per launch from the kernels' own
-counters / HIP-event average duration, on the launch stream), the NN's MFMA roofline, and the CPU
-baseline (the oracle port + the same net on the host cores, bounded sample).
+time, the roofline of the dominant kernel (the NN trunk: executed and algorithmic FLOPs per
+launch / in-situ duration), the search kernels' HBM roofline, the CPU baseline (the oracle port +
+the same net on the host cores, bounded sample) and, at N = 1, the largest single-GPU config
+(C3) and the 6x6 config (C5) measured the same way.
 """
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import sys
@@ -33,11 +39,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}   # dense peaks, same source
+MFMA16_PEAK_TFLOPS = 2500.0      # dense 16-bit (f16/bf16) MFMA peak, same source
 
 
 PRESETS = {   # BASELINE.json configs
-    # lanes: independent game lanes per GPU in one graph (same games; measured best per config)
+    # lanes: independent game lanes per GPU (same games; measured best per config)
     # c1: the reference's own plumbing case (one game, 100 sims, the ModelConfig default 5x128
     # net; config.py:14-15) on one GPU, with the CPU port on the same single game beside it
     "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1),
@@ -48,13 +54,17 @@ PRESETS = {   # BASELINE.json configs
                warmup=0),
     "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2),
 }
+# measured beside the headline in the default N = 1 line (the largest single-GPU config and the
+# 6x6 variant); each is a full workload of its preset over the same --steps
+SUB_CONFIGS = ("c3", "c5")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", choices=sorted(PRESETS), default="c2",
                     help="BASELINE.json workload preset; explicit flags override it")
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without torchrun bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed plies; the default spans a whole 8x8 game (every stage, endgame "
                          "included): the steady-state mix of continuous self-play")
@@ -65,13 +75,7 @@ def parse():
     ap.add_argument("--blocks", type=int, default=None)
     ap.add_argument("--filters", type=int, default=None)
     ap.add_argument("--board", type=int, default=None)
-    ap.add_argument("--nn-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--nn-kernel", choices=["auto", "h2", "split", "resnet", "miopen"],
-                    default="auto",
-                    help="leaf evaluator: h2 (fp32 as a 2-part f16 split, 3 products, MFMA; the "
-                         "auto choice), split (3-part bf16 split, 6 products), resnet (f32 MFMA), "
-                         "miopen")
     ap.add_argument("--instrument-plies", type=int, default=2)
     ap.add_argument("--skip-last-eval", action="store_true",
                     help="leave each search's last batch unevaluated (rvz_search_skip): "
@@ -83,7 +87,7 @@ def parse():
                          "live leaves (mcts.py:544-623 evaluates U; rows of games whose traversal "
                          "ended on a terminal are dead)")
     ap.add_argument("--lanes", type=int, default=None,
-                    help="independent game lanes per GPU, one stream each in one graph "
+                    help="independent game lanes per GPU, one stream each "
                          "(rvz.LaneRunner); the games are the same as with one lane")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="one graph for all lanes with a fork / join per ply (default: one "
@@ -94,24 +98,99 @@ def parse():
     ap.add_argument("--no-stamps", action="store_true",
                     help="no device stamps in the timed graph (roofline from the isolated "
                          "back-to-back launches)")
+    ap.add_argument("--sub-configs", default=None,
+                    help="comma-separated presets measured beside the headline (default at one "
+                         "rank with --config c2: c3,c5; 'none' for none)")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real multi-GPU runs; gloo to rehearse several ranks "
                          "on one device")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks, form the process group and shard the games, print the "
+                         "line without running self-play (launcher check; no GPU needed)")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="stored rocprofv3 PMC passes (FETCH_SIZE / WRITE_SIZE) whose HBM bytes "
+                         "per launch are quoted as roofline.traffic, labelled with their source")
     ap.add_argument("--train-steps", type=int, default=100,
                     help="c4: DDP optimizer steps per iteration (batch --train-batch per rank)")
     ap.add_argument("--train-batch", type=int, default=64,
                     help="c4: per-rank training batch (TrainingConfig.batch_size = 64)")
-    args = ap.parse_args()
-    for k, v in dict(dict(steps=60, warmup=3), **PRESETS[args.config]).items():
-        if getattr(args, k) is None:
-            setattr(args, k, v)
+    args = ap.parse_args(argv)
+    apply_preset(args, args.config)
     return args
 
 
+def apply_preset(args, name):
+    for k, v in dict(dict(steps=60, warmup=3), **PRESETS[name]).items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+
+
+def fail(msg: str, code: int = 2):
+    print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+# ------------------------------------------------------------------------------ ranks
+def launch(args):
+    """`--gpus N` with no launcher around us: start N rank processes of this same command line
+    (children, before any GPU call in this process) and exit with their combined status. Under
+    torchrun (WORLD_SIZE set) or for N = 1 this is a no-op and the process is itself a rank."""
+    if "WORLD_SIZE" in os.environ or args.gpus <= 1:
+        return
+    from rvz import dist as rdist
+    if args.dist_backend == "nccl" and not args.dry_run:
+        avail = torch.cuda.device_count()     # counts devices without initialising HIP
+        if args.gpus > avail:
+            fail(f"--gpus {args.gpus} but only {avail} HIP device(s) visible (backend nccl)")
+    rc = rdist.spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
+    sys.exit(rc)
+
+
+def setup(args):
+    """Join the process group (also at one rank) and pick this rank's device. Returns
+    (rank, world, device, backend); device is None for --dry-run."""
+    import torch.distributed as tdist
+
+    from rvz import dist as rdist
+    rank, local_rank, world = rdist.env_rank_world()
+    if world != args.gpus:
+        fail(f"WORLD_SIZE {world} != --gpus {args.gpus}")
+    backend = args.dist_backend if not args.dry_run else "gloo"
+    device = None
+    if not args.dry_run:
+        n_dev = torch.cuda.device_count()
+        if n_dev < 1:
+            fail("no HIP device")
+        if backend == "nccl" and local_rank >= n_dev:
+            fail(f"LOCAL_RANK {local_rank} has no device ({n_dev} visible, backend nccl)")
+        device = torch.device("cuda", local_rank % n_dev)   # gloo rehearsals may share one GPU
+        torch.cuda.set_device(device)
+    rdist.init(backend, always=True, device=device)
+    if tdist.get_world_size() != args.gpus:
+        fail(f"process group world {tdist.get_world_size()} != --gpus {args.gpus}")
+    return rank, tdist.get_world_size(), device, tdist.get_backend()
+
+
+def dry_run(args, rank, world, backend):
+    import torch.distributed as tdist
+
+    from rvz import dist as rdist
+    shards = [None] * world
+    a, b = rdist.shard_range(args.games * world, rank, world)
+    tdist.all_gather_object(shards, (rank, a, b, os.getpid()))
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher check)", "n_gpus": world,
+                          "rccl_world": world, "dist_backend": backend,
+                          "games_per_gpu": args.games, "global_games": args.games * world,
+                          "shards": [[r, a, b] for r, a, b, _ in shards],
+                          "pids": sorted({p for *_, p in shards})}), flush=True)
+    tdist.destroy_process_group()
+
+
+# ------------------------------------------------------------------------------ measurement
 def make_net(args, device):
     import rvz
     torch.manual_seed(0)
@@ -125,6 +204,7 @@ def instrumented(run, eng, ev, plies):
     are never on while timing; both cover the same launches per ply). Each ply is enqueued
     behind a device-side sleep so the host runs ahead of the GPU and the intervals bracket only
     the kernels. The NN is timed separately (back-to-back calls)."""
+    from rvz import _lib
     nn_calls = 0
 
     def one_ply():
@@ -140,11 +220,8 @@ def instrumented(run, eng, ev, plies):
         run.restart_finished(eng.get_state()[2])
 
     eng.timing_enable(True)
-    trunk_pairs, timer = None, None
-    if getattr(ev, "kernel", None) == "h2":
-        from rvz import _lib
-        trunk_pairs, timer = [], _lib.Timer(2 * plies * eng.n_batches)
-        ev.trunk_events = (timer, trunk_pairs)
+    trunk_pairs, timer = [], _lib.Timer(2 * plies * eng.n_batches)
+    ev.trunk_events = (timer, trunk_pairs)
     for _ in range(plies):
         one_ply()
     ev.trunk_events = None
@@ -167,17 +244,23 @@ def instrumented(run, eng, ev, plies):
     torch.cuda.synchronize(eng.device)
     ms = {"step": t["step"][0], "act": t["act"][0], "nn": a.elapsed_time(b) / 10}
     n = {"step": t["step"][1], "act": t["act"][1], "nn": nn_calls}
-    if getattr(ev, "kernel", None) in ("h2", "split"):   # the trunk launch alone: the dominant kernel
-        ev.trunk_only(eng.leaf_x)
-        a.record(stream)
-        for _ in range(10):
-            ev.trunk_only(eng.leaf_x)
-        b.record(stream)
-        torch.cuda.synchronize(eng.device)
-        ms["nn_trunk"] = a.elapsed_time(b) / 10
+    ms["nn_trunk"] = isolated_trunk_ms(ev, eng.leaf_x)
     if trunk_pairs:   # the trunk launches of the timed plies, in their k_step -> trunk -> heads order
         ms["nn_trunk_in_ply"] = sum(timer.elapsed(i, j) for i, j in trunk_pairs) / len(trunk_pairs)
     return ms, n, {"step": st, "act": act}
+
+
+def isolated_trunk_ms(ev, x):
+    """The trunk launch alone: HIP events over 10 back-to-back full-batch launches."""
+    stream = torch.cuda.current_stream(x.device)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev.trunk_only(x)
+    a.record(stream)
+    for _ in range(10):
+        ev.trunk_only(x)
+    b.record(stream)
+    torch.cuda.synchronize(x.device)
+    return a.elapsed_time(b) / 10
 
 
 def env_bench(device, board=8, n=1 << 23, reps=10):
@@ -196,6 +279,7 @@ def env_bench(device, board=8, n=1 << 23, reps=10):
     status = torch.zeros(n, 4, dtype=torch.int32, device=device)
     status[:, 0] = 1
     plies = torch.randint(0, 41, (n,), generator=g, device=device)
+
     def lowest_bit(x):                                              # index of the lowest set bit
         lsb = x & -x
         f = lsb.to(torch.float64).abs()                             # powers of two are exact
@@ -311,37 +395,227 @@ def cpu_baseline(args, net):
             "env_tree_only_1core": one}
 
 
-def main_c4(args):
+def stored_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC passes (--pmc), quoted only for the
+    configuration they were measured on (C2, 4,096 games), with their source named."""
+    if not (os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096):
+        return None, None
+    try:
+        pmc = json.load(open(args.pmc))
+    except Exception:
+        return None, None
+    b = pmc.get(kernel, {}).get("hbm_bytes_per_launch")
+    if b is None:
+        return None, None
+    src = (f"{os.path.relpath(args.pmc, ROOT)} ({pmc.get('source', 'stored rocprofv3 PMC passes')}"
+           "; not measured in this run)")
+    return b, src
+
+
+def selfplay(args, device, rank, world, full=True):
+    """One workload (args: a resolved preset) on this rank: warm-up, the ply graph(s) captured,
+    `steps` timed replays, the dominant kernel's in-situ roofline. With `full`, also the eager
+    instrumented plies (search kernels' durations and algorithmic bytes). Returns a dict with
+    the measured pieces (rank-local except value / dt, which are whole-job)."""
+    import rvz
+    from rvz import _lib
+    from rvz import dist as rdist
+    from rvz.measure import trunk_spans
+
+    net = make_net(args, device)
+
+    def make_ev():
+        return rvz.LeafEvaluator(net, device=device)
+
+    def make_eng(n):
+        return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
+                          compact_leaves=not args.no_compact)
+
+    first_game = rank * args.games          # global game index space: rank r owns a shard
+    if args.lanes > 1:
+        run = rvz.LaneRunner(make_eng, make_ev, args.games, args.lanes, temperature=1.0,
+                             fused_softmax=True, autoreset=True,
+                             seed_base=args.seed + first_game, seed_stride=args.games * world,
+                             skip_last_eval=args.skip_last_eval)
+        lane0 = run.runners[0]
+        engines = [r.eng for r in run.runners]
+    else:
+        lane0 = run = rvz.SelfPlayRunner(make_eng(args.games), make_ev(), temperature=1.0,
+                                         fused_softmax=True, autoreset=True,
+                                         seed_base=args.seed + first_game,
+                                         seed_stride=args.games * world,
+                                         skip_last_eval=args.skip_last_eval,
+                                         fused_bookkeeping=not args.torch_bookkeeping)
+        engines = [run.eng]
+    eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
+    run.start()
+
+    # warmup: the first ply eager, then capture the ply graph with lane 0's trunk launches
+    # stamping a ring of per-workgroup device wall-clock stamps, one row per launch (the heads
+    # launch advances the ring's device counter): read after the timed replays, the dominant
+    # kernel's duration over every lane-0 launch of the timed region
+    graph_events = []
+    cap_kw = {"free_run": not args.joined_lanes} if args.lanes > 1 else {}
+    warm = max(args.warmup, 0 if args.no_graph else 1)
+    for i in range(warm):
+        if i == 0 and not args.no_graph and not args.no_stamps:
+            run.ply()
+            grid = _lib.load().rvz_resnet_h2_grid(args.board, args.filters, eng.n_games)
+            ring = max(1, args.steps) * eng.n_batches
+            stamps = torch.zeros(ring, grid, 2, dtype=torch.int64, device=device)
+            ctr = torch.zeros(1, dtype=torch.int32, device=device)
+            ev.trunk_stamps = (stamps, ctr)
+            run.capture(**cap_kw)
+            graph_events = [stamps, ctr]
+            ev.trunk_stamps = None
+            continue
+        run.ply()
+        if i == 0 and not args.no_graph:
+            run.capture(**cap_kw)
+    torch.cuda.synchronize(device)
+
+    rows0 = sum(e.rows_total() for e in engines)
+    if graph_events:
+        graph_events[1].zero_()            # the ring starts with the timed region
+    rdist.barrier()
+    torch.cuda.synchronize(device)
+    s0 = int(run.steps.item())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run.ply()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    rdist.barrier()
+    s1 = int(run.steps.item())
+    rows1 = sum(e.rows_total() for e in engines)
+    for e in engines:
+        e.check()
+    total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
+    # leaf rows evaluated per NN call in the timed region (compaction on), else the full batch
+    nn_calls = args.steps * sum(e.n_batches for e in engines)
+    rows = rows1 - rows0 if not args.no_compact else nn_calls * eng.n_games
+    trunk_live = None
+    if graph_events:
+        trunk_live = trunk_spans(graph_events[0], int(graph_events[1].item()))
+        if args.stamps_dump and rank == 0:
+            n_st = min(int(graph_events[1].item()), graph_events[0].shape[0])
+            np.save(args.stamps_dump, graph_events[0][:n_st].cpu().numpy())
+
+    ms = n = bytes_ = None
+    if full:
+        ms, n, bytes_ = instrumented(lane0, eng, ev, args.instrument_plies)
+        eng.check()
+    t_iso = ms["nn_trunk"] if ms else isolated_trunk_ms(ev, eng.leaf_x)
+
+    # roofline of the dominant kernel, the NN trunk k_resnet_h2 (MFMA-bound): FLOPs per row x
+    # rows per launch / launch duration. Executed = the 16-bit MFMA products the kernel issues (3
+    # per fp32 product, stem K 27 -> 32, skipped edge taps); useful = SURVEY §8(d)'s 2 x MACs.
+    fpr, upr = ev.mfma_flops_per_row(), ev.useful_flops_per_row()
+    peak = MFMA16_PEAK_TFLOPS
+    lane_games = eng.n_games
+    iso = {"avg_ms_per_launch": round(t_iso, 4), "rows_per_launch": lane_games,
+           "achieved": round(fpr * lane_games / (t_iso * 1e-3) / 1e12, 2),
+           "frac": round(fpr * lane_games / (t_iso * 1e-3) / 1e12 / peak, 4),
+           "useful_frac": round(upr * lane_games / (t_iso * 1e-3) / 1e12 / peak, 4),
+           "timing": "HIP events over 10 back-to-back launches of one full batch, no other "
+                     "lane running"}
+    if trunk_live:
+        t_tr, rows_tr = trunk_live["ms"], trunk_live["rows"]
+        timing = (f"in the timed region: all {trunk_live['launches']} trunk launches of lane 0, "
+                  "first workgroup start to last end (device s_memrealtime stamps)")
+    else:
+        t_tr, rows_tr, timing = t_iso, lane_games, iso["timing"]
+    ach = fpr * rows_tr / (t_tr * 1e-3) / 1e12
+    ach_u = upr * rows_tr / (t_tr * 1e-3) / 1e12
+    region = fpr * rows / (t1 - t0) / 1e12      # every lane's evaluated rows / timed wall time
+    traffic, traffic_src = (stored_traffic(args, "nn_trunk") if full else (None, None))
+    roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
+            "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4),
+            "flops": "executed 16-bit MFMA FLOPs (mfma_flops_per_row x rows_per_launch)",
+            "mfma_flops_per_row": fpr,
+            "useful_flops_per_row": upr,
+            "useful_achieved": round(ach_u, 2), "useful_frac": round(ach_u / peak, 4),
+            "traffic": traffic, "traffic_source": traffic_src,
+            "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": round(rows_tr, 1),
+            "timing": timing, "isolated": iso,
+            "live_rows_per_launch_timed": round(rows / nn_calls, 1),
+            "timed_region_trunk_tflops": round(region, 2),
+            "timed_region_trunk_frac": round(region / peak, 4),
+            "timed_region_useful_frac": round(upr * rows / (t1 - t0) / 1e12 / peak, 4)}
+    plies_local = s1 - s0
+    out = {"value": value, "dt": dt, "total": total, "roofline": roof, "net": net,
+           "eng": eng, "ev": ev, "lanes": args.lanes,
+           "nn_rows_per_ply": round(rows / max(1, plies_local), 3),
+           "nn_calls_per_ply": sum(e.n_batches for e in engines)}
+    if full:
+        kernels = {}
+        for k in ("step", "act"):
+            per_launch = bytes_[k] / max(1, n[k])
+            kernels[k] = {"avg_us": ms[k] * 1e3, "launches_per_ply": n[k] // args.instrument_plies,
+                          "alg_bytes_per_launch": per_launch,
+                          "achieved_GBs": per_launch / (ms[k] * 1e-3) / 1e9}
+        dom = max(("step", "act"),
+                  key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
+        roof["avg_ms_per_call"] = round(ms["nn"], 4)
+        roof["avg_ms_in_eager_plies"] = (round(ms["nn_trunk_in_ply"], 4)
+                                         if "nn_trunk_in_ply" in ms else None)
+        straffic, ssrc = stored_traffic(args, dom)
+        a = kernels[dom]["achieved_GBs"]
+        out["search_roofline"] = {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(a, 2),
+                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(a / HBM_PEAK_GBS, 5), "traffic": straffic,
+                                  "traffic_source": ssrc}
+        out["kernels"] = {k: {kk: round(vv, 3) for kk, vv in v.items()}
+                          for k, v in kernels.items()}
+        # SURVEY §8d: the env + tree path as a whole — the search kernels' own algorithmic-byte
+        # counters per committed board-step (lane 0's instrumented plies) x the job's rate
+        bps = (bytes_["step"] + bytes_["act"]) / max(1, args.instrument_plies * eng.n_games)
+        out["path_roofline"] = {
+            "what": "env + tree (k_step + k_act algorithmic bytes per board-step, from the "
+                    "kernels' counters) x board-steps/s", "bound": "hbm",
+            "bytes_per_board_step": round(bps, 1), "achieved": round(value * bps / 1e9, 2),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(value * bps / 1e9 / HBM_PEAK_GBS, 5)}
+        # the NN must dominate for "roofline" to name the trunk (else the search kernel)
+        search_ms = kernels[dom]["avg_us"] * kernels[dom]["launches_per_ply"] / 1e3
+        out["nn_dominant"] = t_iso * n["nn"] / max(1, args.instrument_plies) > search_ms
+    return out
+
+
+def sub_config(base, name, device, rank, world):
+    """A preset measured beside the headline: the same harness, its own net and engines."""
+    a = copy.copy(base)
+    for k in ("games", "sims", "blocks", "filters", "board", "lanes"):
+        setattr(a, k, None)
+    a.config = name
+    a.stamps_dump = None
+    apply_preset(a, name)
+    r = selfplay(a, device, rank, world, full=False)
+    out = {"value": round(r["value"], 2), "unit": "board-steps/s",
+           "ms_per_step": round(r["dt"] / a.steps * 1e3, 3), "steps": a.steps,
+           "workload": f"{name}: {a.games} games/GPU x {a.sims} sims, {a.blocks}x{a.filters} "
+                       f"ResNet, {a.board}x{a.board}, {a.lanes} lane(s)",
+           "games_per_gpu": a.games, "sims": a.sims, "nn": f"{a.blocks}x{a.filters}",
+           "board": a.board, "lanes": a.lanes, "nn_rows_per_ply": r["nn_rows_per_ply"],
+           "roofline": r["roofline"]}
+    del r
+    torch.cuda.empty_cache()
+    return out
+
+
+def main_c4(args, rank, world, device):
     """BASELINE.json config 4: self-play + training, one process per GPU (rvz.pipeline;
     reference pipeline.py:114-150). A bench step is one ITERATION: every game of the rank from
     the start position to its end (60 plies, captured ply graph), the device records turned into
     training arrays, then --train-steps DDP steps whose gradient all-reduce runs over RCCL. value
     = board-steps of all ranks / max-over-ranks wall time of the K iterations, training included.
-    The process group is created even at one rank (backend nccl = RCCL), so DDP's all-reduce runs
+    The process group exists even at one rank (backend nccl = RCCL), so DDP's all-reduce runs
     at every N."""
-    import socket
-
     import torch.distributed as tdist
 
-    import rvz
     from rvz import dist as rdist
     from rvz.pipeline import SelfPlayTrainer
 
-    rank, local_rank, world = rdist.env_rank_world()
-    dev_index = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(dev_index)
-    device = torch.device("cuda", dev_index)
-    if not tdist.is_initialized():
-        if world == 1 and "MASTER_PORT" not in os.environ:
-            sk = socket.socket()
-            sk.bind(("127.0.0.1", 0))
-            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
-            sk.close()
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("RANK", str(rank))
-        os.environ.setdefault("WORLD_SIZE", str(world))
-        tdist.init_process_group(backend=args.dist_backend, device_id=device
-                                 if args.dist_backend == "nccl" else None)
     net = make_net(args, device)
     n_params = sum(p.numel() for p in net.parameters())
     spt = SelfPlayTrainer(net, args.games, args.sims, args.batch, 1.0, 1.0, seed=args.seed,
@@ -391,23 +665,19 @@ def main_c4(args):
     ar_ms = rdist.reduce_max(a.elapsed_time(b) / 20)
     # the dominant kernel (the trunk) in isolation: HIP events over 10 back-to-back launches
     ev, eng = spt.evaluator, spt.eng
-    roof = None
-    if ev.kernel == "h2":
-        ev.trunk_only(eng.leaf_x)
-        a.record()
-        for _ in range(10):
-            ev.trunk_only(eng.leaf_x)
-        b.record()
-        torch.cuda.synchronize(device)
-        t_tr = a.elapsed_time(b) / 10
-        fl = ev.mfma_flops_per_row() * eng.n_games
-        ach = fl / (t_tr * 1e-3) / 1e12
-        roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma", "achieved": round(ach, 2),
-                "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
-                "frac": round(ach / MFMA_PEAK_TFLOPS["bf16"], 4), "traffic": None,
-                "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": eng.n_games,
-                "timing": "HIP events over 10 back-to-back full-batch launches after the timed "
-                          "region"}
+    t_tr = isolated_trunk_ms(ev, eng.leaf_x)
+    fl = ev.mfma_flops_per_row() * eng.n_games
+    ach = fl / (t_tr * 1e-3) / 1e12
+    uach = ev.useful_flops_per_row() * eng.n_games / (t_tr * 1e-3) / 1e12
+    roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma", "achieved": round(ach, 2),
+            "peak": MFMA16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / MFMA16_PEAK_TFLOPS, 4),
+            "mfma_flops_per_row": ev.mfma_flops_per_row(),
+            "useful_flops_per_row": ev.useful_flops_per_row(),
+            "useful_frac": round(uach / MFMA16_PEAK_TFLOPS, 4), "traffic": None,
+            "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": eng.n_games,
+            "timing": "HIP events over 10 back-to-back full-batch launches after the timed "
+                      "region"}
     spt.eng.check()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -417,6 +687,7 @@ def main_c4(args):
             "metric": f"self-play board-steps/sec @ {args.sims} sims/move, "
                       f"{args.board}x{args.board} Reversi",
             "value": round(value, 2), "unit": "board-steps/s", "n_gpus": world,
+            "rccl_world": tdist.get_world_size(), "dist_backend": tdist.get_backend(),
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -449,238 +720,65 @@ def main_c4(args):
 
 def main():
     args = parse()
+    launch(args)                               # exits here when it started the ranks itself
+    rank, world, device, backend = setup(args)
+    if args.dry_run:
+        return dry_run(args, rank, world, backend)
     if args.config == "c4":
-        return main_c4(args)
-    import rvz
-    from rvz import dist as rdist
+        return main_c4(args, rank, world, device)
+    import torch.distributed as tdist
 
-    rank, local_rank, world = rdist.env_rank_world()
-    dev_index = local_rank % max(1, torch.cuda.device_count())
-    if world > 1:
-        torch.cuda.set_device(dev_index)
-        rdist.init(args.dist_backend)
-    device = torch.device("cuda", dev_index if world > 1 else torch.cuda.current_device())
-    torch.cuda.set_device(device)
-    nn_dtype = torch.float32 if args.nn_dtype == "fp32" else torch.bfloat16
-
-    net = make_net(args, device)
-    leaf_dtype = torch.float32 if nn_dtype == torch.float32 else torch.bfloat16
-
-    def make_ev():
-        if args.nn_kernel in ("auto", "h2") and nn_dtype == torch.float32:
-            return rvz.LeafEvaluator(net, dtype=nn_dtype, device=device)
-        # A/B alternatives (not the product path): tools/alt/librvz_alt.so
-        sys.path.insert(0, os.path.join(ROOT, "tools", "alt"))
-        from alt_eval import AltEvaluator
-        return AltEvaluator(net, kernel="miopen" if args.nn_kernel in ("auto", "h2")
-                            else args.nn_kernel, dtype=nn_dtype, device=device)
-
-    def make_eng(n):
-        return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
-                          leaf_dtype=leaf_dtype, compact_leaves=not args.no_compact)
-
-    first_game = rank * args.games          # global game index space: rank r owns a shard
-    if args.lanes > 1:
-        run = rvz.LaneRunner(make_eng, make_ev, args.games, args.lanes, temperature=1.0,
-                             fused_softmax=True, autoreset=True,
-                             seed_base=args.seed + first_game, seed_stride=args.games * world,
-                             skip_last_eval=args.skip_last_eval)
-        lane0 = run.runners[0]
-        engines = [r.eng for r in run.runners]
-    else:
-        lane0 = run = rvz.SelfPlayRunner(make_eng(args.games), make_ev(), temperature=1.0,
-                                         fused_softmax=True, autoreset=True,
-                                         seed_base=args.seed + first_game,
-                                         seed_stride=args.games * world,
-                                         skip_last_eval=args.skip_last_eval,
-                                         fused_bookkeeping=not args.torch_bookkeeping)
-        engines = [run.eng]
-    eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
-    run.start()
-
-    # warmup: the first ply eager (MIOpen kernel selection), then capture the ply graph with
-    # lane 0's trunk launches stamping a ring of per-workgroup device wall-clock stamps, one row
-    # per launch (the heads launch advances the ring's device counter): read after the timed
-    # replays, the dominant kernel's duration over every lane-0 launch of the timed region
-    graph_events = []
-    cap_kw = {"free_run": not args.joined_lanes} if args.lanes > 1 else {}
-    warm = max(args.warmup, 0 if args.no_graph else 1)
-    for i in range(warm):
-        if i == 0 and not args.no_graph and ev.kernel == "h2" and not args.no_stamps:
-            from rvz import _lib
-            run.ply()
-            grid = _lib.load().rvz_resnet_h2_grid(args.board, args.filters, eng.n_games)
-            ring = max(1, args.steps) * eng.n_batches
-            stamps = torch.zeros(ring, grid, 2, dtype=torch.int64, device=device)
-            ctr = torch.zeros(1, dtype=torch.int32, device=device)
-            ev.trunk_stamps = (stamps, ctr)
-            run.capture(**cap_kw)
-            graph_events = [stamps, ctr]
-            ev.trunk_stamps = None
-            continue
-        run.ply()
-        if i == 0 and not args.no_graph:
-            run.capture(**cap_kw)
-    torch.cuda.synchronize(device)
-
-    rows0 = sum(e.rows_total() for e in engines)
-    if graph_events:
-        graph_events[1].zero_()            # the ring starts with the timed region
-    rdist.barrier()
-    torch.cuda.synchronize(device)
-    s0 = int(run.steps.item())
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run.ply()
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
-    rdist.barrier()
-    s1 = int(run.steps.item())
-    rows1 = sum(e.rows_total() for e in engines)
-    # leaf rows evaluated per NN call in the timed region (compaction on), else the full batch
-    nn_calls = args.steps * sum(e.n_batches for e in engines)
-    rows_per_call = (rows1 - rows0) / nn_calls if not args.no_compact else float(eng.n_games)
-    # every lane-0 trunk launch of the timed region: first workgroup start to last workgroup end
-    # (100 MHz device clock; end stamp bits 56-63 = the workgroup's evaluated boards)
-    trunk_live = None
-    if graph_events:
-        from rvz.measure import trunk_spans
-        trunk_live = trunk_spans(graph_events[0], int(graph_events[1].item()))
-        if args.stamps_dump and rank == 0:
-            n_st = min(int(graph_events[1].item()), graph_events[0].shape[0])
-            np.save(args.stamps_dump, graph_events[0][:n_st].cpu().numpy())
-    for e in engines:
-        e.check()
-    total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
-
-    ms, n, bytes_ = instrumented(lane0, eng, ev, args.instrument_plies)
-    eng.check()
-    kernels = {}
-    for k in ("step", "act"):
-        per_launch = bytes_[k] / max(1, n[k])
-        kernels[k] = {"avg_us": ms[k] * 1e3, "launches_per_ply": n[k] // args.instrument_plies,
-                      "alg_bytes_per_launch": per_launch,
-                      "achieved_GBs": per_launch / (ms[k] * 1e-3) / 1e9}
-    dom = max(("step", "act"),
-              key=lambda k: kernels[k]["avg_us"] * kernels[k]["launches_per_ply"])
-    pmc = {}
-    if os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096:
-        try:
-            pmc = json.load(open(args.pmc))
-        except Exception:
-            pmc = {}
-    traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
-    lane_games = eng.n_games                # boards per NN launch
-    nn_flops = ev.flops_per_row() * lane_games
-    nn_tflops = nn_flops / (ms["nn"] * 1e-3) / 1e12
-    nn_per_ply = n["nn"] / max(1, args.instrument_plies)
-    split = "nn_trunk" in ms
-    if split:   # roofline of the NN trunk kernel: executed 16-bit MFMA FLOPs per launch / duration
-        fpr = ev.mfma_flops_per_row()
-        mf = fpr * lane_games
-        t_iso = ms["nn_trunk"]
-        peak = MFMA_PEAK_TFLOPS["bf16"]
-        iso = {"avg_ms_per_launch": round(t_iso, 4), "rows_per_launch": lane_games,
-               "achieved": round(mf / (t_iso * 1e-3) / 1e12, 2),
-               "frac": round(mf / (t_iso * 1e-3) / 1e12 / peak, 4),
-               "timing": "HIP events over 10 back-to-back launches of one full batch, no other "
-                         "lane running"}
-        if trunk_live:
-            # in the timed region: every trunk launch of lane 0, first workgroup start to last
-            # workgroup end (device s_memrealtime stamps, 100 MHz), and the rows those launches
-            # evaluated (from the stamps); with lanes > 1 the other lane's kernels share the chip
-            # during these launches, as in rocprofv3's view
-            ach = fpr * trunk_live["rows"] / (trunk_live["ms"] * 1e-3) / 1e12
-            t_tr, rows_tr = trunk_live["ms"], trunk_live["rows"]
-            timing = (f"in the timed region: all {trunk_live['launches']} trunk launches of lane "
-                      "0, first workgroup start to last end (device s_memrealtime stamps)")
-        else:
-            ach, t_tr, rows_tr, timing = iso["achieved"], t_iso, lane_games, iso["timing"]
-        # the whole timed region: trunk MFMA FLOPs of every lane's evaluated rows / wall time
-        region = fpr * (rows1 - rows0 if not args.no_compact else nn_calls * lane_games) / \
-            (t1 - t0) / 1e12
-        nn_roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
-                   "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                   "frac": round(ach / peak, 4),
-                   "traffic": pmc.get("nn_trunk", {}).get("hbm_bytes_per_launch"),
-                   "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": round(rows_tr, 1),
-                   "timing": timing,
-                   "isolated": iso,
-                   # compacted batches: the timed region's launches evaluate this many live rows
-                   # on average (the endgame's terminal traversals need none)
-                   "live_rows_per_launch_timed": round(rows_per_call, 1),
-                   "timed_region_trunk_tflops": round(region, 2),
-                   "timed_region_trunk_frac": round(region / peak, 4),
-                   # fence-less event pairs around each trunk launch of the eager instrumented
-                   # plies (lane 0 alone)
-                   "avg_ms_in_eager_plies": (round(ms["nn_trunk_in_ply"], 4)
-                                             if "nn_trunk_in_ply" in ms else None),
-                   "mfma_flops_per_row": fpr,
-                   "fp32_equiv_tflops_isolated": round(nn_flops / (t_iso * 1e-3) / 1e12, 2)}
-    else:
-        nn_roof = {"kernel": "rvz_resnet_fwd_f32" if ev.kernel == "resnet" else "miopen",
-                   "bound": "mfma", "achieved": round(nn_tflops, 2),
-                   "peak": MFMA_PEAK_TFLOPS[args.nn_dtype], "unit": "TFLOP/s",
-                   "frac": round(nn_tflops / MFMA_PEAK_TFLOPS[args.nn_dtype], 4), "traffic": None}
-    nn_roof["avg_ms_per_call"] = round(ms["nn"], 4)
-    nn_roof["calls_per_ply"] = round(nn_per_ply, 2)
-    search_ms_per_ply = kernels[dom]["avg_us"] * kernels[dom]["launches_per_ply"] / 1e3
-    nn_dominant = ms.get("nn_trunk", ms["nn"]) * nn_per_ply > \
-        search_ms_per_ply
-
+    r = selfplay(args, device, rank, world, full=True)
+    value, dt, net = r["value"], r["dt"], r["net"]
+    subs = {}
+    names = (args.sub_configs.split(",") if args.sub_configs not in (None, "none") else
+             (SUB_CONFIGS if args.sub_configs is None and world == 1 and args.config == "c2"
+              else ()))
+    for name in names:
+        if name and name != args.config:
+            subs[name] = sub_config(args, name, device, rank, world)
     envb = env_bench(device, args.board) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, net)
 
     if rank == 0:
-        ach = kernels[dom]["achieved_GBs"]
-        search_roof = {"kernel": f"k_{dom}", "bound": "hbm", "achieved": round(ach, 2),
-                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic}
-        # the env + tree path as a whole — the search kernels' own algorithmic-byte
-        # counters per committed board-step (lane 0's instrumented plies) x the job's board-steps/s
-        bps = (bytes_["step"] + bytes_["act"]) / max(1, args.instrument_plies * eng.n_games)
-        path_roof = {"what": "env + tree (k_step + k_act algorithmic bytes per board-step, from "
-                             "the kernels' counters) x board-steps/s", "bound": "hbm",
-                     "bytes_per_board_step": round(bps, 1),
-                     "achieved": round(value * bps / 1e9, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(value * bps / 1e9 / HBM_PEAK_GBS, 5)}
+        roof = r["roofline"]
+        nn_dom = r["nn_dominant"]
         out = {
             "metric": f"self-play board-steps/sec @ {args.sims} sims/move, "
                       f"{args.board}x{args.board} Reversi",
             "value": round(value, 2), "unit": "board-steps/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "n_gpus": world, "rccl_world": tdist.get_world_size(), "dist_backend": backend,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u64 rules + f32 NN" + ({"h2": " (fp32 as 2-part f16 split on MFMA)",
-                                               "split": " (fp32 as 3-part bf16 split on MFMA)"}
-                                              .get(ev.kernel, "") if split else ""),
+            "dtype": "u64 rules + f32 NN (fp32 as 2-part f16 split on MFMA)",
             "data": "synthetic (start position, per-game seeds, random-init net)",
             "config": {"workload": f"{args.config}: {args.games} games/GPU x {args.sims} sims, "
                                    f"{args.blocks}x{args.filters} ResNet, {args.board}x{args.board}",
                        "games_per_gpu": args.games, "global_games": args.games * world,
                        "sims": args.sims, "batch": args.batch,
-                       "nn": f"{args.blocks}x{args.filters}", "nn_dtype": args.nn_dtype,
-                       "nn_kernel": {"h2": "rvz_resnet_fwd_h2", "split": "rvz_resnet_fwd_split",
-                                     "resnet": "rvz_resnet_fwd_f32"}
-                       .get(getattr(ev, "kernel", ""), "miopen+rvz_nn_bias_act"),
+                       "nn": f"{args.blocks}x{args.filters}", "nn_kernel": "rvz_resnet_fwd_h2",
                        "graph": not args.no_graph, "lanes": args.lanes,
                        "lane_graphs": ("joined" if args.joined_lanes else "free")
                        if args.lanes > 1 else None,
                        "skip_last_eval": args.skip_last_eval,
                        "parallelism": f"games sharded x{world}"},
-            # the dominant kernel of a ply (by time per ply) carries "roofline"; the other side
-            # of the ply (NN vs search) is reported beside it
-            "roofline": nn_roof if nn_dominant else search_roof,
-            "search_roofline" if nn_dominant else "nn_roofline":
-                search_roof if nn_dominant else nn_roof,
-            "kernels": {k: {kk: round(vv, 3) for kk, vv in v.items()} for k, v in kernels.items()},
-            "path_roofline": path_roof,
+            "nn_rows_per_ply": r["nn_rows_per_ply"],
+            "nn_calls_per_ply": r["nn_calls_per_ply"],
+            # the dominant kernel of a ply (by time per ply) carries "roofline"
+            "roofline": roof if nn_dom else r["search_roofline"],
+            "search_roofline" if nn_dom else "nn_roofline":
+                r["search_roofline"] if nn_dom else roof,
+            "kernels": r["kernels"],
+            "path_roofline": r["path_roofline"],
             "env_roofline": envb,
+            "configs": subs or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    tdist.destroy_process_group()
 
 
 if __name__ == "__main__":

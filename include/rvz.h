@@ -197,7 +197,11 @@ int rvz_resnet_heads_fc(int32_t board, const float *work, int32_t n, const float
  * work: rvz_resnet_work_size(n) floats (16-byte aligned); work[n * 192] (zero it before the first
  * use) is set to 1 (never cleared by the kernel) if an activation reached the f16 range limit
  * 65520, i.e. the outputs are not valid; words n * 192 + 2, 3 hold the trunk's 64-bit board-unit
- * counter (units dealt to workgroups in start order; any initial value below 2^63). */
+ * counter (units dealt to workgroups in start order; any initial value below 2^63). A misaligned
+ * work returns RVZ_EINVAL. A workspace must not be shared by launches that can run concurrently
+ * (two streams, or one buffer reused across overlapping launches): every launch claims its
+ * board units from the counter, and interleaved claims would skip or repeat units silently.
+ * Give each stream (each lane) its own workspace. */
 int64_t rvz_resnet_h2_size(int32_t filters, int32_t blocks);
 int rvz_resnet_h2_weights(const float *params, int32_t filters, int32_t blocks, uint16_t *blob,
                           void *hip_stream);

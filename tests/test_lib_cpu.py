@@ -97,3 +97,18 @@ def test_alt_library_matches_its_header():
     assert exported == decl, exported ^ decl
     alt_eval.load()
     assert not decl & set(declared_symbols())
+
+
+def test_evaluator_entry_points_reject_a_misaligned_workspace():
+    """the trunk's 64-bit unit-counter atomic and the heads' f32x4 row copies need a
+    16-byte aligned workspace; a misaligned one is RVZ_EINVAL at the C-ABI (argument checks run
+    before any HIP call, so this needs no GPU), never a device fault."""
+    import rvz
+    lib = rvz.load()
+    EINVAL = -22
+    params, blob, x, out = 0x10000, 0x20000, 0x30000, 0x40000   # never dereferenced
+    for work in (0x50004, 0x50008):
+        assert lib.rvz_resnet_trunk_h2(8, x, 64, params, blob, 64, 6, work, None) == EINVAL
+        assert lib.rvz_resnet_heads_fc(8, work, 64, params, 64, 6, out, out, None) == EINVAL
+        assert lib.rvz_resnet_fwd_h2(8, x, 64, params, blob, 64, 6, work, out, out,
+                                     None) == EINVAL

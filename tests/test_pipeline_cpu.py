@@ -140,3 +140,6 @@ def test_records_to_ddp_two_ranks_identical_nets():
     for k in sd0:                 # weights via the all-reduce, BN buffers via sync_buffers
         assert np.array_equal(sd0[k], sd1[k]), k
     assert res[0][2]["steps"] == 4 and np.isfinite(res[0][2]["train/loss"])
+    # the loss dict is the job's: the mean over ranks, identical on every rank
+    assert res[0][2]["train/loss"] == res[1][2]["train/loss"]
+    assert res[0][2]["train/value_loss"] == res[1][2]["train/value_loss"]
