@@ -128,6 +128,29 @@ def apply_preset(args, name):
             setattr(args, k, v)
 
 
+_LINE_FD = None     # the real stdout: only the JSON line goes there (see quiet_stdout)
+
+
+def quiet_stdout():
+    """Keep stdout for the one JSON line: native libraries print banners to fd 1 (RCCL's version
+    block at communicator init, gloo's connection log), so fd 1 is pointed at stderr for the rest
+    of the process and emit() writes the line to the saved descriptor."""
+    global _LINE_FD
+    if _LINE_FD is None:
+        sys.stdout.flush()
+        _LINE_FD = os.dup(1)
+        os.dup2(2, 1)
+
+
+def emit(obj):
+    line = (json.dumps(obj) + "\n").encode()
+    if _LINE_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_LINE_FD, line)
+
+
 def fail(msg: str, code: int = 2):
     print(f"bench.py: {msg}", file=sys.stderr, flush=True)
     sys.exit(code)
@@ -182,11 +205,11 @@ def dry_run(args, rank, world, backend):
     a, b = rdist.shard_range(args.games * world, rank, world)
     tdist.all_gather_object(shards, (rank, a, b, os.getpid()))
     if rank == 0:
-        print(json.dumps({"metric": "dry-run (launcher check)", "n_gpus": world,
-                          "rccl_world": world, "dist_backend": backend,
-                          "games_per_gpu": args.games, "global_games": args.games * world,
-                          "shards": [[r, a, b] for r, a, b, _ in shards],
-                          "pids": sorted({p for *_, p in shards})}), flush=True)
+        emit({"metric": "dry-run (launcher check)", "n_gpus": world, "rccl_world": world,
+              "dist_backend": backend, "games_per_gpu": args.games,
+              "global_games": args.games * world,
+              "shards": [[r, a, b] for r, a, b, _ in shards],
+              "pids": sorted({p for *_, p in shards})})
     tdist.destroy_process_group()
 
 
@@ -714,13 +737,14 @@ def main_c4(args, rank, world, device):
             "train_loss": [round(r["train/loss"], 4) for r in its],
             "roofline": roof, "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     tdist.destroy_process_group()
 
 
 def main():
     args = parse()
     launch(args)                               # exits here when it started the ranks itself
+    quiet_stdout()
     rank, world, device, backend = setup(args)
     if args.dry_run:
         return dry_run(args, rank, world, backend)
@@ -777,7 +801,7 @@ def main():
             "configs": subs or None,
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     tdist.destroy_process_group()
 
 

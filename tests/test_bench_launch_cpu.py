@@ -29,7 +29,7 @@ def _run(args, env=None, timeout=240):
 def test_bench_gpus_n_starts_n_ranks(n, games):
     r = _run(["--gpus", str(n), "--dist-backend", "gloo", "--dry-run", "--games", str(games)])
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]   # gloo logs aside
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]   # native logs go to stderr
     assert len(lines) == 1, r.stdout            # rank 0 only
     d = json.loads(lines[0])
     assert d["n_gpus"] == n and d["rccl_world"] == n and d["dist_backend"] == "gloo"
