@@ -97,7 +97,28 @@ struct View {  // kernel argument: device pointers + sizes
     int32_t* row_of;  // [G]
     unsigned long long* live_total;  // running sum of the live counts (rows handed out)
     int E, NS;
+    // NN-output memo across consecutive searches (rvz_search_memo; memo = 0: off). The pool has
+    // two halves of E expansion blocks; a search writes one half while the previous search's
+    // tree stays readable in the other. bval[g][b]: the NN value of the node expanded into block
+    // b; carry[g]: the link (LINK_* below) of the child the last move went to, or LINK_NONE.
+    int memo;
+    uint32_t* carry;  // [G]
+    float* bval;      // [G][2E]
 };
+
+// A link names an expanded node of the previous search's tree (the same position as the new
+// node it is attached to): its index, child count and block. Stored in the `c` (cached UCB) field
+// of an unvisited node, which the reference formula never reads while N == 0 (mcts.py:96-97;
+// the first backup overwrites it with "not cached"), and in carry[g] for the next root.
+// LINK_NONE is the "not cached" NaN every other node carries; a link is < 2^28, never a NaN.
+constexpr uint32_t LINK_NONE = 0x7fc00000u;
+__host__ __device__ constexpr uint32_t link_pack(int node, int nchild, int block) {
+    return (uint32_t)node | ((uint32_t)nchild << 14) | ((uint32_t)block << 21);
+}
+__device__ __forceinline__ bool link_ok(uint32_t l) { return l < (1u << 28); }
+__device__ __forceinline__ int link_node(uint32_t l) { return (int)(l & 0x3fffu); }
+__device__ __forceinline__ int link_nchild(uint32_t l) { return (int)((l >> 14) & 127u); }
+__device__ __forceinline__ int link_block(uint32_t l) { return (int)((l >> 21) & 127u); }
 
 // ERR_NN: an evaluator handed the expand a non-finite value or probability (an overflowed or
 // broken leaf evaluator must not feed the tree silently; the reference would play on with NaN)
@@ -305,6 +326,7 @@ __device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lan
         meta[leaf] = nlm;
         v.nexp[g] = x.e + 1;
         v.pend[g] = 0;
+        if (v.memo) v.bval[(size_t)g * 2 * v.E + x.e] = x.val;   // the next search's memo
     }
     if (leaf == 0 && root_meta) *root_meta = nlm;
     // the path nodes are not among the nodes written above: no ordering needed before the RMW
@@ -335,12 +357,64 @@ __device__ __forceinline__ void backup_visits_only(const View& v, int g, int lan
     if (v.stats) ab += 8ull + 4ull * plen + 8ull * plen;
 }
 
+// A leaf whose position the previous search of this game already expanded (link lk: that node
+// of the previous tree, kept in the other half of the pool): _process_batch pass 2 (mcts.py:
+// 600-623) with that expansion's NN output instead of a new evaluation. An h2 row's outputs
+// depend only on the position (test_h2_live_rows), so the priors (the softmax of the row at the
+// legal squares, which are the old node's children in row-major order, exactly the squares the
+// same position yields here) and the value are bitwise what the evaluator would return for this
+// leaf now. The children get their own links (the old children that were expanded too); the
+// value is backed up `copies` times at once, where the evaluated leaf's backup would run at the
+// head of the next launch — the same point of the batch (after its terminal backups).
+template <int BS>
+__device__ __forceinline__ int memo_expand_backup(const View& v, int g, int lane, int leaf,
+                                                  uint32_t lm, int path_reg, int plen,
+                                                  uint32_t lk, int copies,
+                                                  unsigned long long& ab) {
+    constexpr int NSQ = Geo<BS>::NSQ;
+    Node* nodes = v.nodes + (size_t)g * v.M;
+    uint32_t* meta = v.meta + (size_t)g * v.M;
+    const int nch = link_nchild(lk), ob = 1 + link_block(lk) * NSQ;
+    // one round trip: the old children rows, the old node's value and the expansion counter
+    Node oc;
+    uint32_t ocm = 0;
+    if (lane < nch) {
+        oc = nodes[ob + lane];
+        ocm = meta[ob + lane];
+    }
+    const float val = v.bval[(size_t)g * 2 * v.E + link_block(lk)];
+    const int e = v.nexp[g];
+    const int base = 1 + e * NSQ;
+    if (base + NSQ > v.M) {
+        if (lane == 0) atomicOr(v.err, ERR_POOL);
+        return -1;
+    }
+    if (lane < nch) {
+        Node c;
+        c.n = 0; c.w = 0.0f; c.p = oc.p;
+        const bool expd = m_nchild(ocm) > 0 && !m_term(ocm);
+        c.c = __uint_as_float(expd ? link_pack(ob + lane, m_nchild(ocm), m_block(ocm))
+                                   : LINK_NONE);
+        nodes[base + lane] = c;
+        meta[base + lane] = meta_pack(m_sq(ocm), 3 - m_turn(lm));
+    }
+    if (lane == 0) {
+        meta[leaf] = lm | ((uint32_t)nch << 11) | ((uint32_t)e << 18);
+        v.nexp[g] = e + 1;
+        v.bval[(size_t)g * 2 * v.E + e] = val;
+    }
+    ab += 20ull * nch + 8 + 20ull * nch + 12 + 32ull * plen;
+    // this walk's UCB-cache stores to path nodes come before the read-modify-write
+    return backup_path(nodes, path_reg, plen, val, copies, lane, true);
+}
+
 // select: mcts.py:348-386 for one batch of `bsz` traversals + _process_batch pass 1 (:561-585).
 // root / root_meta / root_n were loaded (or produced by the expand phase) by the caller.
 template <int BS, typename XT>
 __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int first, int bsz,
                                              int eb,
                                              const GameS& root, uint32_t root_meta, int root_n,
+                                             uint32_t carry,
                                              XT* __restrict__ leaf_x, int32_t* __restrict__ need,
                                              unsigned long long& ab) {
     constexpr int NSQ = Geo<BS>::NSQ;
@@ -349,12 +423,15 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
     if (first) {  // new root (mcts.py:334-341): prior 1.0, turn = side to move
         root_meta = meta_pack(0, root.side);
         root_n = 0;
+        // memo: this search's blocks go to the half the previous tree (where the carried node
+        // lives) does not use; without a carried node, half 0
+        const int half = (v.memo && link_ok(carry) && (link_node(carry) - 1) / NSQ < v.E) ? 1 : 0;
         if (lane == 0) {
             Node r;
             r.n = 0; r.w = 0.0f; r.p = 1.0f; r.c = __int_as_float(0x7fc00000);
             nodes[0] = r;
             meta[0] = root_meta;
-            v.nexp[g] = 0;
+            v.nexp[g] = half * v.E;
         }
         const uint64_t rl = root.over ? 0ull : legal_wave<BS>(mine(root), theirs(root), lane);
         if (lane == 0) v.root_legal[g] = rl;
@@ -370,6 +447,8 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
             GameS sim = root;
             int depth = 0, node = 0, parent_n = root_n;
             uint32_t m = root_meta;
+            // memo link of the node the walk ends on (the root's: the carried node)
+            uint32_t lk = first ? carry : LINK_NONE;
             path_reg = 0;  // lane 0 holds the root
             // per level d (in lane d): the chosen child's index, its turn for scoring, the best
             // other child's score and index (-1: none) — the terminal fast path below
@@ -415,6 +494,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 node = base + ci;
                 m = (uint32_t)lane_bcast((int)cm, ci);
                 parent_n = lane_bcast(c.n, ci);
+                if (v.memo) lk = (uint32_t)lane_bcast(__float_as_int(c.c), ci);
                 ++depth;
                 if (depth >= PATH_CAP) {  // unreachable when ceil(sims/batch) <= 64 (checked)
                     if (lane == 0) atomicOr(v.err, ERR_PATH);
@@ -491,6 +571,14 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
                 if (remaining == 0) break;
                 continue;
             }
+            if (v.memo && link_ok(lk) && !truncated) {
+                // the previous search evaluated this position: expand it from that output, no
+                // NN row (the position has legal moves, so it is not terminal)
+                const int rn = memo_expand_backup<BS>(v, g, lane, node, m, path_reg, depth + 1,
+                                                      lk, remaining, ab);
+                if (rn >= 0) root_n = rn;
+                break;
+            }
             WT_NOW(tl0);
             // the leaf's position: the path's moves on the root's game (a truncated path, an
             // error already flagged, replays its first PATH_CAP - 1 moves)
@@ -565,11 +653,13 @@ __global__ __launch_bounds__(256) RVZ_STEP_ATTR void k_step(View v, int expand, 
     const int g = blockIdx.x * WPB + (threadIdx.x >> 6);
     if (g >= v.G) return;
     const GameS root = load_game(v, g);
-    uint32_t root_meta = 0;
+    uint32_t root_meta = 0, carry = LINK_NONE;
     int root_n = 0;
     if (!first) {
         root_meta = v.meta[(size_t)g * v.M];
         root_n = v.nodes[(size_t)g * v.M].n;
+    } else if (v.memo) {
+        carry = v.carry[g];
     }
     unsigned long long ab_e = 0, ab_s = 0;
     WT_NOW(te0);
@@ -579,7 +669,8 @@ __global__ __launch_bounds__(256) RVZ_STEP_ATTR void k_step(View v, int expand, 
         if (rn >= 0) root_n = rn;
     }
     WT_ADD(0, te0);
-    select_phase<BS, XT>(v, g, lane, first, bsz, eb, root, root_meta, root_n, leaf_x, need, ab_s);
+    select_phase<BS, XT>(v, g, lane, first, bsz, eb, root, root_meta, root_n, carry, leaf_x, need,
+                         ab_s);
     if (v.stats && lane == 0) v.stats[g] += ab_s + ab_e;  // per-game slot: no contention
 }
 
@@ -676,6 +767,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? 6
         if (lane == 0) {
             prow[NSQ] = 0.0;
             out_idx[g] = -2;
+            if (v.memo) v.carry[g] = LINK_NONE;
             if (v.stats) v.stats[(size_t)v.G + g] += ab + 32 + 8ull * NPOL + 4;
         }
         return;
@@ -754,6 +846,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? 6
         make_move_wave<BS>(gm, idx == NSQ ? -1 : idx, lane);  // (-1, -1) for the pass index
         if (lane == 0) store_game(v, g, gm);
     }
+    if (v.memo && lane == 0) {
+        // the child the move went to (its position is the next search's root), if this search
+        // expanded it: the next search's root takes that expansion's NN output (memo_expand_backup)
+        uint32_t cl = LINK_NONE;
+        const uint32_t m0 = v.meta[(size_t)g * v.M];
+        const uint64_t V = v.root_legal[g];
+        if (apply && idx < NSQ && m_nchild(m0) > 0 && ((V >> idx) & 1ull)) {
+            const int c = 1 + m_block(m0) * NSQ + __popcll(V & ((1ull << idx) - 1ull));
+            const uint32_t cm = v.meta[(size_t)g * v.M + c];
+            if (m_nchild(cm) > 0 && !m_term(cm)) cl = link_pack(c, m_nchild(cm), m_block(cm));
+        }
+        v.carry[g] = cl;
+    }
     if (v.stats && lane == 0)  // state r/(w), root meta + children N, p row + idx, rng
         v.stats[(size_t)v.G + g] += ab + 32ull + (apply ? 32 : 0) + 12 +
                                     4ull * m_nchild(v.meta[(size_t)g * v.M]) + 8ull * NPOL + 4 + 16;
@@ -794,6 +899,7 @@ __device__ __forceinline__ void reset_game(const View& v, int g, int lane, uint3
         store_game(v, g, st);
         v.rng_pos[g] = 0;
         v.pend[g] = 0;
+        v.carry[g] = LINK_NONE;   // a new game: nothing to carry into its first search
     }
 }
 
@@ -1002,7 +1108,7 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     e->NSQ = bs * bs;
     e->NPOL = e->NSQ + 1;
     e->E = E;
-    e->M = 1 + E * e->NSQ;
+    e->M = 1 + 2 * E * e->NSQ;   // root + two halves of E expansion blocks (the memo's two trees)
     e->v.E = E;
     e->v.NS = (cfg->n_games + RVZ_LIVE_STRIPE - 1) / RVZ_LIVE_STRIPE;
     e->v.live = nullptr;
@@ -1028,6 +1134,9 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     v.rng_u = dalloc<double>(e, (size_t)G * RNG_DRAWS);
     v.rng_pos = dalloc<int32_t>(e, G);
     v.err = dalloc<int32_t>(e, 1);
+    v.memo = 0;
+    v.carry = dalloc<uint32_t>(e, G);
+    v.bval = dalloc<float>(e, (size_t)G * 2 * E);
     e->stats_buf = dalloc<unsigned long long>(e, 3 * (size_t)G);
     v.stats = nullptr;
     for (void* p : e->allocs)
@@ -1039,6 +1148,7 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     s = s == hipSuccess ? hipMemset(v.root_legal, 0, sizeof(uint64_t) * G) : s;
     s = s == hipSuccess ? hipMemset(v.leaf_meta, 0, sizeof(uint32_t) * G) : s;
     s = s == hipSuccess ? hipMemset(v.path, 0, sizeof(int32_t) * G * PATH_CAP) : s;
+    s = s == hipSuccess ? hipMemsetD32(v.carry, LINK_NONE, G) : s;
     if (s == hipSuccess) s = hipDeviceSynchronize();
     if (s != hipSuccess) {
         g_create_error = std::string("device init: ") + hipGetErrorString(s);
@@ -1127,9 +1237,18 @@ int rvz_env_get(rvz_engine* e, uint64_t* black, uint64_t* white, int32_t* status
     return RVZ_OK;
 }
 
+// The memo's carried links hold only while each search follows the previous one's move
+// (rvz_act with apply): a position set or moved from the host, or an abandoned search, drops them.
+static int memo_drop(rvz_engine* e) {
+    if (!e->v.memo) return RVZ_OK;
+    RVZ_HIP(hipMemsetD32Async(e->v.carry, LINK_NONE, e->v.G, e->stream), e);
+    return RVZ_OK;
+}
+
 int rvz_env_set(rvz_engine* e, const uint64_t* black, const uint64_t* white, const int32_t* status) {
     if (!e || !black || !white || !status) return RVZ_EINVAL;
     e->pending = 0;
+    if (memo_drop(e) != RVZ_OK) return RVZ_EHIP;
     const size_t G = e->v.G;
     RVZ_HIP(hipMemcpyAsync(e->v.black, black, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
     RVZ_HIP(hipMemcpyAsync(e->v.white, white, G * 8, hipMemcpyDeviceToDevice, e->stream), e);
@@ -1183,6 +1302,7 @@ int rvz_env_legal(rvz_engine* e, uint64_t* out) {
 int rvz_env_apply(rvz_engine* e, const int32_t* sq, int32_t* ok) {
     const Range trace_range("rvz.env.apply");
     if (!e) return RVZ_EINVAL;
+    if (memo_drop(e) != RVZ_OK) return RVZ_EHIP;
     int r = rvz_board_apply(e->BS, e->v.G, e->v.black, e->v.white, e->v.status, sq, ok, e->stream);
     if (r != RVZ_OK) e->err = "rvz_env_apply launch failed";
     else e->counters[1] += 1;
@@ -1193,6 +1313,7 @@ int rvz_env_apply(rvz_engine* e, const int32_t* sq, int32_t* ok) {
 int rvz_search_begin(rvz_engine* e) {
     const Range trace_range("rvz.search.begin");
     if (!e) return RVZ_EINVAL;
+    if (e->searching && e->next_batch > 0 && memo_drop(e) != RVZ_OK) return RVZ_EHIP;
     e->next_batch = 0;
     e->searching = 1;
     if (e->v.live && e->live_dirty) {   // an abandoned search left counts behind
@@ -1292,6 +1413,23 @@ int rvz_search_compact(rvz_engine* e, int32_t on) {
     e->v.row_of = on ? e->live_buf + (size_t)e->E * e->v.NS * RVZ_LIVE_PITCH : nullptr;
     e->v.live_total = on ? e->live_total : nullptr;
     return RVZ_OK;
+}
+
+int rvz_search_memo(rvz_engine* e, int32_t on) {
+    if (!e) return RVZ_EINVAL;
+    if (e->pending || (e->searching && e->next_batch > 0)) {
+        e->err = "rvz_search_memo inside a search";
+        return RVZ_EINVAL;
+    }
+    e->v.memo = 1;             // so that memo_drop clears the links either way
+    if (memo_drop(e) != RVZ_OK) return RVZ_EHIP;
+    e->v.memo = on ? 1 : 0;
+    return RVZ_OK;
+}
+
+int rvz_search_memo_reset(rvz_engine* e) {
+    if (!e) return RVZ_EINVAL;
+    return memo_drop(e);
 }
 
 int rvz_search_rows_total(rvz_engine* e, int64_t* out) {
@@ -1498,7 +1636,9 @@ int rvz_tree_export(rvz_engine* e, void* nodes_out, uint32_t* meta_out) {
 int rvz_footprint(const rvz_engine* e, int64_t* bytes_tree, int64_t* bytes_env) {
     if (!e) return RVZ_EINVAL;
     const int64_t G = e->v.G;
-    if (bytes_tree) *bytes_tree = G * e->M * (int64_t)(sizeof(Node) + sizeof(uint32_t)) + G * (PATH_CAP * 4 + 4 * 4 + 8);
+    if (bytes_tree)
+        *bytes_tree = G * e->M * (int64_t)(sizeof(Node) + sizeof(uint32_t)) +
+                      G * (PATH_CAP * 4 + 4 * 4 + 8) + G * (4 + 2 * e->E * 4);   // + memo
     if (bytes_env) *bytes_env = G * (8 + 8 + 16) + G * (RNG_DRAWS * 8 + 4);
     return RVZ_OK;
 }

@@ -61,6 +61,8 @@ SIGNATURES = {
     "rvz_resnet_fwd_h2_ex": (C.c_int, [C.c_int32, _P, C.c_int32, _P, _P, C.c_int32, C.c_int32,
                                        _P, _P, _P, _P, _P]),
     "rvz_search_compact": (C.c_int, [_P, C.c_int32]),
+    "rvz_search_memo": (C.c_int, [_P, C.c_int32]),
+    "rvz_search_memo_reset": (C.c_int, [_P]),
     "rvz_search_live_count": (C.c_void_p, [_P]),
     "rvz_search_rows_total": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "rvz_timer_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),

@@ -36,7 +36,8 @@ def to_unsigned64(x: int) -> int:
 class Engine:
     def __init__(self, n_games: int, num_simulations: int = 800, batch_size: int = 64,
                  c_puct: float = 1.0, board_size: int = 8, device=None,
-                 leaf_dtype: torch.dtype = torch.float32, compact_leaves: bool = False):
+                 leaf_dtype: torch.dtype = torch.float32, compact_leaves: bool = False,
+                 memo: bool = False):
         if not torch.cuda.is_available():
             raise RvzError("rvz needs a HIP device (MI355X); there is no CPU fallback")
         self.lib = _lib.load()
@@ -73,6 +74,9 @@ class Engine:
         self.compact_leaves = False
         if compact_leaves:
             self.compact(True)
+        self.memo_on = False
+        if memo:
+            self.memo(True)
 
     # ------------------------------------------------------------------ plumbing
     def __del__(self):
@@ -223,6 +227,21 @@ class Engine:
         Same visits, p and moves as the uncompacted search."""
         self._call("rvz_search_compact", int(bool(on)))
         self.compact_leaves = bool(on)
+
+    def memo(self, on: bool = True):
+        """NN-output memo across consecutive searches (rvz_search_memo): a leaf whose position
+        the game's previous search expanded takes that expansion's priors and value instead of
+        a new evaluation (the reference re-evaluates it: it rebuilds the tree every move,
+        mcts.py:334). Same visits, p and moves; fewer evaluated rows. The evaluator must be
+        row-deterministic and unchanged between searches: memo_reset() after new weights."""
+        self._stream()
+        self._call("rvz_search_memo", int(bool(on)))
+        self.memo_on = bool(on)
+
+    def memo_reset(self):
+        """Forget the carried expansions (new evaluator weights); graph-capturable."""
+        self._stream()
+        self._call("rvz_search_memo_reset")
 
     def live_count(self) -> int:
         """Device address of the int32 live-row count of the most recently issued batch."""

@@ -36,7 +36,7 @@ class SelfPlayTrainer:
                  train_steps: Optional[int] = None, train_batch: int = 64, lr: float = 1e-3,
                  weight_decay: float = 1e-4, gradient_clip: float = 1.0,
                  graph: bool = True, compact_leaves: bool = True, lr_milestones=(),
-                 lr_gamma: float = 0.1):
+                 lr_gamma: float = 0.1, memo: bool = True):
         self.model = model.eval()
         self.device = next(model.parameters()).device
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -50,7 +50,7 @@ class SelfPlayTrainer:
         self.evaluator = LeafEvaluator(model)
         bs = int(getattr(model, "board_size", 8))
         self.eng = Engine(games, num_simulations, batch_size, c_puct, board_size=bs,
-                          device=self.device, compact_leaves=compact_leaves)
+                          device=self.device, compact_leaves=compact_leaves, memo=memo)
         self.max_plies = bs * bs - 4
         self.runner = SelfPlayRunner(self.eng, self.evaluator, temperature, record=True,
                                      max_plies=self.max_plies,
@@ -88,6 +88,7 @@ class SelfPlayTrainer:
         self.trainer.scheduler_step()          # pipeline.py:131, once per iteration
         self.model.eval()
         self.evaluator.refresh()
+        self.eng.memo_reset()                  # the memo holds the previous net's outputs
         return out
 
     def run_iteration(self) -> Dict[str, float]:

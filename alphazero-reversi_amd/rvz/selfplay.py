@@ -261,12 +261,16 @@ class SelfPlay:
 
     def _play(self, num_games: int) -> List[Dict]:
         # compacted leaf batches: only the live leaves are evaluated (as _process_batch does);
-        # the games are identical either way
+        # the NN-output memo (Engine.memo) with the default evaluator, whose rows depend only on
+        # the position; the games are identical either way
+        from .network import LeafEvaluator
         bs = self.board_size
         eng = Engine(num_games, self.args.get("num_simulations", 800),
                      self.args.get("batch_size", 64), self.args.get("c_puct", 1.0),
                      board_size=bs, device=self.device,
-                     compact_leaves=bool(self.args.get("compact_leaves", True)))
+                     compact_leaves=bool(self.args.get("compact_leaves", True)),
+                     memo=bool(self.args.get("memo", isinstance(self.evaluator, LeafEvaluator)
+                                             and self.args.get("fused_softmax", True))))
         if hasattr(self.evaluator, "bind"):
             self.evaluator.bind(eng)
         max_plies = bs * bs - 4         # every ply places a disc (passes are inside make_move)

@@ -80,6 +80,12 @@ def parse(argv=None):
     ap.add_argument("--skip-last-eval", action="store_true",
                     help="leave each search's last batch unevaluated (rvz_search_skip): "
                          "bit-identical games, one NN call fewer per move; off for the headline")
+    ap.add_argument("--no-memo", action="store_true",
+                    help="no NN-output memo across consecutive searches (rvz_search_memo): every "
+                         "leaf the previous search already evaluated is evaluated again, as the "
+                         "reference does (it rebuilds the tree every move, mcts.py:334)")
+    ap.add_argument("--no-memo-ab", action="store_true",
+                    help="skip the memo-off measurement beside the headline")
     ap.add_argument("--torch-bookkeeping", action="store_true",
                     help="per-ply counting / autoreset as torch ops instead of rvz_env_autoreset")
     ap.add_argument("--no-compact", action="store_true",
@@ -452,7 +458,7 @@ def selfplay(args, device, rank, world, full=True):
 
     def make_eng(n):
         return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
-                          compact_leaves=not args.no_compact)
+                          compact_leaves=not args.no_compact, memo=not args.no_memo)
 
     first_game = rank * args.games          # global game index space: rank r owns a shard
     if args.lanes > 1:
@@ -643,7 +649,8 @@ def main_c4(args, rank, world, device):
     n_params = sum(p.numel() for p in net.parameters())
     spt = SelfPlayTrainer(net, args.games, args.sims, args.batch, 1.0, 1.0, seed=args.seed,
                           train_steps=args.train_steps, train_batch=args.train_batch,
-                          graph=not args.no_graph, compact_leaves=not args.no_compact)
+                          graph=not args.no_graph, compact_leaves=not args.no_compact,
+                          memo=not args.no_memo)
     # warm-up (untimed): one eager ply, the ply graph captured, two DDP steps on stand-in data
     run = spt.runner
     run.start()
@@ -754,6 +761,22 @@ def main():
 
     r = selfplay(args, device, rank, world, full=True)
     value, dt, net = r["value"], r["dt"], r["net"]
+    memo_ab = None
+    if not args.no_memo and not args.no_memo_ab and not args.no_compact:
+        # the same workload with the memo off (the reference's evaluation count): the games are
+        # identical (tests/test_gpu_memo.py), so the row difference is the memo's hits
+        a = copy.copy(args)
+        a.no_memo, a.stamps_dump = True, None
+        off = selfplay(a, device, rank, world, full=False)
+        memo_ab = {"memo_off_value": round(off["value"], 2),
+                   "memo_off_ms_per_step": round(off["dt"] / args.steps * 1e3, 3),
+                   "memo_off_nn_rows_per_ply": off["nn_rows_per_ply"],
+                   "memo_hits_per_ply": round(off["nn_rows_per_ply"] - r["nn_rows_per_ply"], 3),
+                   "memo_hit_rate": round(1 - r["nn_rows_per_ply"] /
+                                          max(1e-9, off["nn_rows_per_ply"]), 4),
+                   "speedup": round(value / off["value"], 4)}
+        del off
+        torch.cuda.empty_cache()
     subs = {}
     names = (args.sub_configs.split(",") if args.sub_configs not in (None, "none") else
              (SUB_CONFIGS if args.sub_configs is None and world == 1 and args.config == "c2"
@@ -787,10 +810,11 @@ def main():
                        "graph": not args.no_graph, "lanes": args.lanes,
                        "lane_graphs": ("joined" if args.joined_lanes else "free")
                        if args.lanes > 1 else None,
-                       "skip_last_eval": args.skip_last_eval,
+                       "skip_last_eval": args.skip_last_eval, "memo": not args.no_memo,
                        "parallelism": f"games sharded x{world}"},
             "nn_rows_per_ply": r["nn_rows_per_ply"],
             "nn_calls_per_ply": r["nn_calls_per_ply"],
+            "memo": memo_ab if memo_ab else {"on": not args.no_memo},
             # the dominant kernel of a ply (by time per ply) carries "roofline"
             "roofline": roof if nn_dom else r["search_roofline"],
             "search_roofline" if nn_dom else "nn_roofline":

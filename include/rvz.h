@@ -129,6 +129,21 @@ int rvz_search_skip(rvz_engine *e);
  * uncompacted search. */
 int rvz_search_compact(rvz_engine *e, int32_t on);
 const int32_t *rvz_search_live_count(const rvz_engine *e);
+/* NN-output memo across consecutive searches (on != 0; off by default). The reference rebuilds
+ * the tree at every move (mcts.py:334), so the next search's root — the child the move went to —
+ * and often some of its descendants are positions this game's previous search already expanded
+ * from an NN evaluation. With the memo on, such a leaf is expanded from that earlier output (the
+ * priors of its children and its value, kept in the other half of the node pool) instead of
+ * being queued for the evaluator: need[g] = 0 and no leaf row for it. A leaf evaluator's row
+ * outputs must depend only on the position (true of rvz_resnet_fwd_h2 and any deterministic
+ * per-row net), and the net must not change between the two searches: call
+ * rvz_search_memo_reset after new weights. Visits, p and moves are identical to the search
+ * without the memo (tests/test_gpu_memo.py); it changes only how many rows are evaluated.
+ * The carried links are dropped automatically by rvz_env_reset / rvz_env_autoreset (per game),
+ * rvz_env_set, rvz_env_apply, rvz_act without apply and an abandoned search. Not inside a
+ * search. */
+int rvz_search_memo(rvz_engine *e, int32_t on);
+int rvz_search_memo_reset(rvz_engine *e);
 /* Host int64: the live rows of every batch of every search completed by rvz_act since
  * compaction was first enabled (0 if never enabled); synchronises the engine stream. */
 int rvz_search_rows_total(rvz_engine *e, int64_t *out /* host */);
