@@ -25,7 +25,7 @@ def _play(memo, G, sims, plies, board=8, net=None, compact=True, skip=False, lan
 
     if lanes > 1:
         run = rvz.LaneRunner(make_eng, lambda: rvz.LeafEvaluator(net), G, lanes, autoreset=True,
-                             seed_base=seed_base, skip_last_eval=skip)
+                             seed_base=seed_base, seed_stride=1000, skip_last_eval=skip)
         engines = [r.eng for r in run.runners]
     else:
         run = rvz.SelfPlayRunner(make_eng(G), rvz.LeafEvaluator(net), autoreset=True,
