@@ -77,15 +77,21 @@ def parse(argv=None):
     ap.add_argument("--board", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--instrument-plies", type=int, default=2)
+    ap.add_argument("--evals", choices=("lazy", "memo", "reference"), default="lazy",
+                    help="which NN rows are evaluated (the games are bit-identical in all three, "
+                         "tests/test_gpu_memo.py): 'reference' = every leaf of every batch, as the "
+                         "reference does (it rebuilds the tree every move, mcts.py:334); 'memo' = "
+                         "a leaf the game's previous search already evaluated takes that output "
+                         "(rvz_search_memo); 'lazy' = memo, and each search's last batch is left "
+                         "unevaluated (rvz_search_skip: nothing reads its output in that search) "
+                         "and evaluated by a later search only if one reaches its position")
     ap.add_argument("--skip-last-eval", action="store_true",
-                    help="leave each search's last batch unevaluated (rvz_search_skip): "
-                         "bit-identical games, one NN call fewer per move; off for the headline")
+                    help="leave each search's last batch unevaluated (also without the memo)")
     ap.add_argument("--no-memo", action="store_true",
-                    help="no NN-output memo across consecutive searches (rvz_search_memo): every "
-                         "leaf the previous search already evaluated is evaluated again, as the "
-                         "reference does (it rebuilds the tree every move, mcts.py:334)")
-    ap.add_argument("--no-memo-ab", action="store_true",
-                    help="skip the memo-off measurement beside the headline")
+                    help="no NN-output memo (with --evals lazy: the last batch is still skipped "
+                         "only if --skip-last-eval)")
+    ap.add_argument("--no-evals-ab", "--no-memo-ab", dest="no_evals_ab", action="store_true",
+                    help="skip the measurements of the other --evals modes beside the headline")
     ap.add_argument("--torch-bookkeeping", action="store_true",
                     help="per-ply counting / autoreset as torch ops instead of rvz_env_autoreset")
     ap.add_argument("--no-compact", action="store_true",
@@ -125,7 +131,18 @@ def parse(argv=None):
                     help="c4: per-rank training batch (TrainingConfig.batch_size = 64)")
     args = ap.parse_args(argv)
     apply_preset(args, args.config)
+    args.force_skip = args.skip_last_eval
+    if args.no_memo:
+        args.evals = "reference"
+    set_evals(args, args.evals)
     return args
+
+
+def set_evals(args, mode):
+    """--evals mode -> the engine switches (skip_last_eval stays on if asked for explicitly)."""
+    args.evals = mode
+    args.no_memo = mode == "reference"
+    args.skip_last_eval = mode == "lazy" or getattr(args, "force_skip", False)
 
 
 def apply_preset(args, name):
@@ -761,22 +778,24 @@ def main():
 
     r = selfplay(args, device, rank, world, full=True)
     value, dt, net = r["value"], r["dt"], r["net"]
-    memo_ab = None
-    if not args.no_memo and not args.no_memo_ab and not args.no_compact:
-        # the same workload with the memo off (the reference's evaluation count): the games are
-        # identical (tests/test_gpu_memo.py), so the row difference is the memo's hits
-        a = copy.copy(args)
-        a.no_memo, a.stamps_dump = True, None
-        off = selfplay(a, device, rank, world, full=False)
-        memo_ab = {"memo_off_value": round(off["value"], 2),
-                   "memo_off_ms_per_step": round(off["dt"] / args.steps * 1e3, 3),
-                   "memo_off_nn_rows_per_ply": off["nn_rows_per_ply"],
-                   "memo_hits_per_ply": round(off["nn_rows_per_ply"] - r["nn_rows_per_ply"], 3),
-                   "memo_hit_rate": round(1 - r["nn_rows_per_ply"] /
-                                          max(1e-9, off["nn_rows_per_ply"]), 4),
-                   "speedup": round(value / off["value"], 4)}
-        del off
-        torch.cuda.empty_cache()
+    evals_ab = {}
+    if not args.no_evals_ab and not args.no_compact:
+        # the same workload with the other --evals modes: the games are identical
+        # (tests/test_gpu_memo.py, test_bench_configuration_at_full_size_plays_the_plain_games), so
+        # the row differences are the memo's hits and the deferred last batches
+        for mode in ("reference", "memo", "lazy"):
+            if mode == args.evals:
+                continue
+            a = copy.copy(args)
+            set_evals(a, mode)
+            a.stamps_dump = None
+            o = selfplay(a, device, rank, world, full=False)
+            evals_ab[mode] = {"value": round(o["value"], 2),
+                              "ms_per_step": round(o["dt"] / args.steps * 1e3, 3),
+                              "nn_rows_per_ply": o["nn_rows_per_ply"],
+                              "speedup_of_headline": round(value / o["value"], 4)}
+            del o
+            torch.cuda.empty_cache()
     subs = {}
     names = (args.sub_configs.split(",") if args.sub_configs not in (None, "none") else
              (SUB_CONFIGS if args.sub_configs is None and world == 1 and args.config == "c2"
@@ -810,11 +829,15 @@ def main():
                        "graph": not args.no_graph, "lanes": args.lanes,
                        "lane_graphs": ("joined" if args.joined_lanes else "free")
                        if args.lanes > 1 else None,
-                       "skip_last_eval": args.skip_last_eval, "memo": not args.no_memo,
+                       "evals": args.evals, "skip_last_eval": args.skip_last_eval,
+                       "memo": not args.no_memo,
                        "parallelism": f"games sharded x{world}"},
             "nn_rows_per_ply": r["nn_rows_per_ply"],
             "nn_calls_per_ply": r["nn_calls_per_ply"],
-            "memo": memo_ab if memo_ab else {"on": not args.no_memo},
+            "evals_ab": evals_ab or None,
+            "nn_rows_frac_of_reference": (round(r["nn_rows_per_ply"] /
+                                                max(1e-9, evals_ab["reference"]["nn_rows_per_ply"]),
+                                                4) if "reference" in evals_ab else None),
             # the dominant kernel of a ply (by time per ply) carries "roofline"
             "roofline": roof if nn_dom else r["search_roofline"],
             "search_roofline" if nn_dom else "nn_roofline":

@@ -117,7 +117,8 @@ def test_split_kernel_6x6_matches_module(blocks, filters, n):
 
 
 @pytest.mark.parametrize("kernel", ["resnet", "split", "h2"])
-@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 4096), (10, 128, 515), (1, 64, 3), (0, 128, 2)])
+@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 4096), (10, 128, 515), (5, 128, 257), (1, 64, 3),
+                                              (0, 128, 2)])
 def test_resnet_kernel_matches_module(kernel, blocks, filters, n):
     """rvz_resnet_fwd_f32 (f32 MFMA), rvz_resnet_fwd_split (fp32 as 3 bf16 parts) and
     rvz_resnet_fwd_h2 (fp32 as 2 f16 parts), whole forward, vs the nn.Module (fp32): fp32-class
@@ -136,7 +137,7 @@ def test_resnet_kernel_matches_module(kernel, blocks, filters, n):
     assert (v - vr).abs().max().item() <= 2e-3
 
 
-@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 512), (10, 128, 128)])
+@pytest.mark.parametrize("blocks,filters,n", [(6, 64, 512), (10, 128, 128), (5, 128, 128)])
 def test_split_error_is_fp32_class(blocks, filters, n):
     """Error against an fp64 evaluation of the same module: the split kernels' (3 bf16 parts, 2
     f16 parts) must be of the order of the fp32 paths' (f32 MFMA kernel, PyTorch fp32) — not

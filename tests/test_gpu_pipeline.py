@@ -35,6 +35,44 @@ def test_selfplay_trainer_iterations_use_the_trained_net(tmp_path):
     assert sum(len(g["states"]) for g in games) == data["states"].shape[0]
 
 
+def test_c4_shaped_iteration_over_rccl_world1(tmp_path):
+    """C4's shape at world 1 (BASELINE.json configs[3]: 10x128 net, 800 sims; 2,048 games on the
+    one GPU instead of 32,768): one SelfPlayTrainer iteration with its DDP steps' gradients going
+    through RCCL (backend "nccl"), then the next iteration's captured self-play must equal an
+    eager SelfPlay of the trained net with the same seeds (reference pipeline.py:114-150)."""
+    import socket
+    import torch.distributed as dist
+    import rvz
+    from rvz.pipeline import SelfPlayTrainer
+    G, S = 2048, 800
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        net = rvz.AlphaZeroNetwork(8, 10, 128).cuda()
+        init = {k: v.clone() for k, v in net.state_dict().items()}
+        spt = SelfPlayTrainer(net, G, num_simulations=S, seed=11, train_steps=20, train_batch=64)
+        assert spt.distributed and spt.world == 1
+        r0 = spt.run_iteration()
+        assert r0["board_steps"] == r0["samples"] >= 9 * G and r0["steps"] == 20
+        assert np.isfinite(r0["train/loss"])
+        moved = max((net.state_dict()[k].float() - init[k].float()).abs().max().item()
+                    for k in init if init[k].is_floating_point())
+        assert moved > 1e-4                     # the DDP steps changed the weights
+        data = spt.generate()                   # iteration 1: graph replays, memo reset
+    finally:
+        dist.destroy_process_group()
+    sp = rvz.SelfPlay(net, {"num_simulations": S, "seed": 11 + G, "save_dir": str(tmp_path)})
+    games = sp.generate_games(G)
+    t = sp.training_tensors()
+    assert sum(len(g["states"]) for g in games) == data["states"].shape[0]
+    assert torch.equal(t["states"], data["states"])
+    assert torch.equal(t["policy_targets"], data["policy_targets"])
+    assert torch.equal(t["value_targets"], data["value_targets"])
+
+
 def test_ddp_trainer_over_rccl_world1_equals_plain_training():
     """DDPTrainer with a torch.distributed process group on the 'nccl' backend (RCCL on ROCm) at
     world size 1: every step's gradients go through DDP's bucketed RCCL all-reduce, and the

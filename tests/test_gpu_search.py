@@ -515,17 +515,21 @@ def test_compact_api_errors():
     assert rc == -22                                      # RVZ_EINVAL: counter without a ring
 
 
-def test_bench_configuration_at_full_size_plays_the_plain_games():
-    """The bench's C2 configuration at full size (4,096 games x 800 sims, 6x64 net; 3 free-running
-    lane graphs of 1,366 / 1,365 / 1,365 games, compacted leaf batches) against the plain path (one runner, every row
-    evaluated, eager) over a whole game and its restarts: every ply's moves and the final boards,
-    statuses and ply counters are identical."""
+@pytest.mark.parametrize("n_lanes,memo,skip", [(3, False, False), (2, True, True)])
+def test_bench_configuration_at_full_size_plays_the_plain_games(n_lanes, memo, skip):
+    """The bench's C2 configuration at full size (4,096 games x 800 sims, 6x64 net; free-running
+    lane graphs of games split in order (3 lanes: 1,366 / 1,365 / 1,365), compacted leaf batches;
+    the headline's form: 2 lanes, the NN-output memo and the last batch left to the memo) against
+    the plain path (one runner, every row evaluated, no memo, every batch evaluated, eager) over a
+    whole game and its restarts: every ply's moves and the final boards, statuses and ply counters
+    are identical."""
     import rvz
     G, S, plies = 4096, 800, 64
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 6, 64).cuda().eval()
-    lanes = rvz.LaneRunner(lambda n: rvz.Engine(n, S, 64, compact_leaves=True),
-                           lambda: rvz.LeafEvaluator(net), G, 3, autoreset=True, seed_base=42)
+    lanes = rvz.LaneRunner(lambda n: rvz.Engine(n, S, 64, compact_leaves=True, memo=memo),
+                           lambda: rvz.LeafEvaluator(net), G, n_lanes, autoreset=True,
+                           seed_base=42, skip_last_eval=skip)
     plain = rvz.SelfPlayRunner(rvz.Engine(G, S, 64), rvz.LeafEvaluator(net), autoreset=True,
                                seed_base=42)
     lanes.start()
