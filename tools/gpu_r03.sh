@@ -24,6 +24,6 @@ fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o bench \
-    -- python bench.py --no-cpu-baseline --sub-configs none ${BENCH_ARGS:-} > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
+    -- python bench.py --no-cpu-baseline --sub-configs none --no-evals-ab ${BENCH_ARGS:-} > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err"
 rc=$?; echo "prof_rc=$rc"; exit $rc
 fi
