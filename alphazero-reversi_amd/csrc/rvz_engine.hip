@@ -729,12 +729,15 @@ __device__ __forceinline__ double np_power(double x, double e) {
     return rvz_pow::pow_cr(x, e);
 }
 
+#ifndef RVZ_ACT_WPE
+#define RVZ_ACT_WPE 6
+#endif
 // act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action); optionally preceded
 // by the last batch's pending expand + backup.
 template <int BS>
 // 8x8: <= 80 VGPRs (6 waves per SIMD), so a k_act wave fits on a SIMD beside two trunk waves
 // (2 x 216); the 6x6 form would spill under that cap
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? 6 : 1))) void k_act(View v, int expand, const float* __restrict__ policy,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? RVZ_ACT_WPE : 1))) void k_act(View v, int expand, const float* __restrict__ policy,
                                              int is_logits, const float* __restrict__ value,
                                              double temperature, const double* __restrict__ uo,
                                              int apply, int32_t* __restrict__ out_idx,
@@ -745,11 +748,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? 6
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = blockIdx.x * WPB + wid;
     if (g >= v.G) return;
-    // the search's leaf batches are all consumed (their NN calls precede this launch)
+    // the search's leaf batches are all consumed (their NN calls precede this launch); the rows
+    // of a skipped last batch (expand == 2, rvz_search_skip) were handed out but not evaluated
     if (v.live && lane == 0) {
+        const int counted = expand == 2 ? (v.E - 1) * v.NS : v.E * v.NS;
         for (int i = g; i < v.E * v.NS; i += v.G) {
             const int c = v.live[(size_t)i * RVZ_LIVE_PITCH];
-            if (c) atomicAdd(v.live_total, (unsigned long long)c);
+            if (c && i < counted) atomicAdd(v.live_total, (unsigned long long)c);
             v.live[(size_t)i * RVZ_LIVE_PITCH] = 0;
         }
     }

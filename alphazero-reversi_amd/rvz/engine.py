@@ -251,7 +251,8 @@ class Engine:
         return int(a)
 
     def rows_total(self) -> int:
-        """Live rows handed to the evaluator over all completed searches (compaction on)."""
+        """Live rows evaluated over all completed searches (compaction on; the rows of a last
+        batch left by skip_last_eval are not counted)."""
         out = C.c_int64()
         self._call("rvz_search_rows_total", C.byref(out))
         return int(out.value)

@@ -110,14 +110,21 @@ class SelfPlayRunner:
         self._seed32.copy_(self.seeds.bitwise_and(0xFFFFFFFF).to(torch.int32))
         self.eng.reset_device(self._seed32, self._mask)
 
-    def capture(self):
-        """Capture one ply into a HIP graph (call after at least one eager ply warmed MIOpen)."""
+    def capture(self, plies: int = 1):
+        """Capture `plies` plies into one HIP graph (call after at least one eager ply warmed the
+        kernels); ply() then replays them all (plies_per_call)."""
+        if plies < 1 or (plies > 1 and self.record):
+            raise ValueError("plies >= 1; a recording runner captures one ply per graph")
         torch.cuda.synchronize(self.eng.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._body()
+            for _ in range(plies):
+                self._body()
         self.graph = g
+        self.plies_per_call = int(plies)
         torch.cuda.synchronize(self.eng.device)
+
+    plies_per_call = 1        # plies one ply() call plays (a captured multi-ply graph: more)
 
     def ply(self):
         if self.graph is not None:
@@ -202,10 +209,13 @@ class LaneRunner:
         for s in self.streams:
             main.wait_stream(s)
 
-    def capture(self, free_run: bool = False):
+    def capture(self, free_run: bool = False, plies: int = 1):
         """One graph holding every lane with a fork / join per ply, or (free_run) one graph per
         lane replayed on the lane's own stream: the lanes then drift freely against each other
-        (no per-ply join bubble) and meet only at join() / a device synchronisation."""
+        (no per-ply join bubble) and meet only at join() / a device synchronisation. `plies`
+        plies go into each graph (ply() then plays them all): fewer graph launch boundaries."""
+        if plies < 1:
+            raise ValueError("plies >= 1")
         dev = self.runners[0].eng.device
         torch.cuda.synchronize(dev)
         if free_run:
@@ -213,14 +223,19 @@ class LaneRunner:
             for r, s in zip(self.runners, self.streams):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):
-                    r._body()
+                    for _ in range(plies):
+                        r._body()
                 self.lane_graphs.append(g)
         else:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._body()
+                for _ in range(plies):
+                    self._body()
             self.graph = g
+        self.plies_per_call = int(plies)
         torch.cuda.synchronize(dev)
+
+    plies_per_call = 1
 
     def ply(self):
         if self.lane_graphs:

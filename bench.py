@@ -101,6 +101,9 @@ def parse(argv=None):
     ap.add_argument("--lanes", type=int, default=None,
                     help="independent game lanes per GPU, one stream each "
                          "(rvz.LaneRunner); the games are the same as with one lane")
+    ap.add_argument("--plies-per-graph", type=int, default=1,
+                    help="plies captured into each lane's HIP graph (one replay plays them all; "
+                         "--steps must be a multiple)")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="one graph for all lanes with a fork / join per ply (default: one "
                          "graph per lane on its own stream, no per-ply join; +0.9%% at C2)")
@@ -502,6 +505,10 @@ def selfplay(args, device, rank, world, full=True):
     # kernel's duration over every lane-0 launch of the timed region
     graph_events = []
     cap_kw = {"free_run": not args.joined_lanes} if args.lanes > 1 else {}
+    ppg = 1 if args.no_graph else args.plies_per_graph
+    if args.steps % ppg:
+        raise SystemExit(f"--steps {args.steps} is not a multiple of --plies-per-graph {ppg}")
+    cap_kw["plies"] = ppg
     warm = max(args.warmup, 0 if args.no_graph else 1)
     for i in range(warm):
         if i == 0 and not args.no_graph and not args.no_stamps:
@@ -527,10 +534,16 @@ def selfplay(args, device, rank, world, full=True):
     torch.cuda.synchronize(device)
     s0 = int(run.steps.item())
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    t_enq = []
+    for _ in range(args.steps // ppg):     # one replay plays ppg plies
         run.ply()
+        t_enq.append(time.perf_counter())
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
+    if os.environ.get("RVZ_BENCH_ENQ"):
+        iv = np.diff(np.array([t0] + t_enq)) * 1e3
+        print(f"[bench] {args.config}: host enqueue ms per ply: {np.round(iv, 3).tolist()}; "
+              f"device total {(t1 - t0) * 1e3:.1f} ms", file=sys.stderr)
     rdist.barrier()
     s1 = int(run.steps.item())
     rows1 = sum(e.rows_total() for e in engines)
@@ -538,7 +551,9 @@ def selfplay(args, device, rank, world, full=True):
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
     # leaf rows evaluated per NN call in the timed region (compaction on), else the full batch
-    nn_calls = args.steps * sum(e.n_batches for e in engines)
+    # (a last batch left to the memo, --evals lazy, is not an NN call)
+    calls_per_search = [e.n_batches - (1 if args.skip_last_eval else 0) for e in engines]
+    nn_calls = args.steps * sum(calls_per_search)
     rows = rows1 - rows0 if not args.no_compact else nn_calls * eng.n_games
     trunk_live = None
     if graph_events:
@@ -593,7 +608,11 @@ def selfplay(args, device, rank, world, full=True):
     out = {"value": value, "dt": dt, "total": total, "roofline": roof, "net": net,
            "eng": eng, "ev": ev, "lanes": args.lanes,
            "nn_rows_per_ply": round(rows / max(1, plies_local), 3),
-           "nn_calls_per_ply": sum(e.n_batches for e in engines)}
+           "nn_calls_per_ply": sum(calls_per_search),
+           # host time to enqueue the timed plies (graph replays): below ms_per_step, the device
+           # never waits for the host
+           "host_enqueue_ms_per_step": round((t_enq[-1] - t0) / max(1, args.steps) * 1e3, 3),
+           "plies_per_graph": ppg}
     if full:
         kernels = {}
         for k in ("step", "act"):
@@ -691,6 +710,10 @@ def main_c4(args, rank, world, device):
     its = [spt.run_iteration() for _ in range(args.steps)]
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
+    if os.environ.get("RVZ_BENCH_ENQ"):
+        iv = np.diff(np.array([t0] + t_enq)) * 1e3
+        print(f"[bench] {args.config}: host enqueue ms per ply: {np.round(iv, 3).tolist()}; "
+              f"device total {(t1 - t0) * 1e3:.1f} ms", file=sys.stderr)
     rdist.barrier()
     steps = sum(r["board_steps"] for r in its)
     total, dt, value = rdist.aggregate_rate(steps, t1 - t0)
@@ -834,6 +857,7 @@ def main():
                        "parallelism": f"games sharded x{world}"},
             "nn_rows_per_ply": r["nn_rows_per_ply"],
             "nn_calls_per_ply": r["nn_calls_per_ply"],
+            "host_enqueue_ms_per_step": r["host_enqueue_ms_per_step"],
             "evals_ab": evals_ab or None,
             "nn_rows_frac_of_reference": (round(r["nn_rows_per_ply"] /
                                                 max(1e-9, evals_ab["reference"]["nn_rows_per_ply"]),

@@ -144,8 +144,9 @@ const int32_t *rvz_search_live_count(const rvz_engine *e);
  * search. */
 int rvz_search_memo(rvz_engine *e, int32_t on);
 int rvz_search_memo_reset(rvz_engine *e);
-/* Host int64: the live rows of every batch of every search completed by rvz_act since
- * compaction was first enabled (0 if never enabled); synchronises the engine stream. */
+/* Host int64: the live rows of every evaluated batch of every search completed by rvz_act since
+ * compaction was first enabled (0 if never enabled; a batch left by rvz_search_skip is not
+ * counted); synchronises the engine stream. */
 int rvz_search_rows_total(rvz_engine *e, int64_t *out /* host */);
 /* {move: child.visit_count} (mcts.py:406-407) as int32 [n_games, S*S+1] */
 int rvz_search_visits(rvz_engine *e, int32_t *out);

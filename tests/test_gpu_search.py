@@ -442,10 +442,8 @@ def test_compacted_leaves_play_the_same_games(board, live_aware, skip):
     for k, (x, y) in enumerate(zip(ta, tb)):
         for u, v in zip(x, y):
             assert torch.equal(u, v), k
-    # rows_total counts the skipped last batch's live rows too (queued, not evaluated)
-    assert rows[0] >= rows[1] and rows[0] < G * plies * 2
-    if not skip:
-        assert rows[0] == rows[1]
+    # rows_total counts the evaluated rows: a skipped last batch's rows are not among them
+    assert rows[0] == rows[1] and rows[0] < G * plies * 2
 
 
 def test_free_running_lanes_play_the_same_games():
