@@ -36,6 +36,7 @@
 #include <vector>
 
 #include "../../include/rvz.h"
+#include "rvz_h2.hip.h"
 #include "rvz_pow.hip.h"
 #include "rvz_rules.hip.h"
 #include "rvz_trace.h"
@@ -411,7 +412,7 @@ __device__ __forceinline__ int memo_expand_backup(const View& v, int g, int lane
 // select: mcts.py:348-386 for one batch of `bsz` traversals + _process_batch pass 1 (:561-585).
 // root / root_meta / root_n were loaded (or produced by the expand phase) by the caller.
 template <int BS, typename XT>
-__device__ __forceinline__ void select_phase(const View& v, int g, int lane, int first, int bsz,
+__device__ __forceinline__ int select_phase(const View& v, int g, int lane, int first, int bsz,
                                              int eb,
                                              const GameS& root, uint32_t root_meta, int root_n,
                                              uint32_t carry,
@@ -632,6 +633,7 @@ __device__ __forceinline__ void select_phase(const View& v, int g, int lane, int
         v.plen[g] = plen;
     }
     ab += 12;
+    return copies;   // the queued copies of the batch's NN row (0: no row)
 }
 
 // One search round: the previous batch's expand + backup (when a submit is pending), then the
@@ -729,35 +731,18 @@ __device__ __forceinline__ double np_power(double x, double e) {
     return rvz_pow::pow_cr(x, e);
 }
 
-#ifndef RVZ_ACT_WPE
-#define RVZ_ACT_WPE 6
-#endif
-// act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action); optionally preceded
-// by the last batch's pending expand + backup.
+// act for one game (one wave): the search's pending expand (expand 1) or visit-count backup
+// (expand 2), then get_action_probs' tail and the move; returns the sampled index (-2: the game
+// was over). s: NPOL + 7 doubles of this wave's LDS.
 template <int BS>
-// 8x8: <= 80 VGPRs (6 waves per SIMD), so a k_act wave fits on a SIMD beside two trunk waves
-// (2 x 216); the 6x6 form would spill under that cap
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? RVZ_ACT_WPE : 1))) void k_act(View v, int expand, const float* __restrict__ policy,
-                                             int is_logits, const float* __restrict__ value,
-                                             double temperature, const double* __restrict__ uo,
-                                             int apply, int32_t* __restrict__ out_idx,
-                                             double* __restrict__ out_p) {
+__device__ __forceinline__ int act_game(const View& v, int g, int lane, double* s, int expand,
+                                        const float* __restrict__ policy, int is_logits,
+                                        const float* __restrict__ value, double temperature,
+                                        const double* __restrict__ uo, int apply,
+                                        int32_t* __restrict__ out_idx, double* __restrict__ out_p,
+                                        bool* over_after = nullptr) {
     constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
     constexpr int NMAIN = NPOL - NPOL % 8;
-    __shared__ double sp[WPB][NPOL + 7];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int g = blockIdx.x * WPB + wid;
-    if (g >= v.G) return;
-    // the search's leaf batches are all consumed (their NN calls precede this launch); the rows
-    // of a skipped last batch (expand == 2, rvz_search_skip) were handed out but not evaluated
-    if (v.live && lane == 0) {
-        const int counted = expand == 2 ? (v.E - 1) * v.NS : v.E * v.NS;
-        for (int i = g; i < v.E * v.NS; i += v.G) {
-            const int c = v.live[(size_t)i * RVZ_LIVE_PITCH];
-            if (c && i < counted) atomicAdd(v.live_total, (unsigned long long)c);
-            v.live[(size_t)i * RVZ_LIVE_PITCH] = 0;
-        }
-    }
     unsigned long long ab = 0;
     if (expand == 1) {
         const ExpIn x = expand_load<BS>(v, g, lane, policy, value);
@@ -775,13 +760,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? R
             if (v.memo) v.carry[g] = LINK_NONE;
             if (v.stats) v.stats[(size_t)v.G + g] += ab + 32 + 8ull * NPOL + 4;
         }
-        return;
+        if (over_after) *over_after = true;
+        return -2;
     }
     const int n = root_visits<BS>(v, g, lane);
     const int total = wave_sum_i(n);
     double p = (lane < NSQ && total > 0) ? (double)n / (double)total : 0.0;
     double ppass = 0.0;
-    double* s = sp[wid];
     if (temperature > 0.0 && __any(p != 0.0)) {
         const double ex = 1.0 / temperature;
         const double t = lane < NSQ ? np_power(p, ex) : 0.0;
@@ -851,6 +836,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? R
         make_move_wave<BS>(gm, idx == NSQ ? -1 : idx, lane);  // (-1, -1) for the pass index
         if (lane == 0) store_game(v, g, gm);
     }
+    if (over_after) *over_after = gm.over != 0;
     if (v.memo && lane == 0) {
         // the child the move went to (its position is the next search's root), if this search
         // expanded it: the next search's root takes that expansion's NN output (memo_expand_backup)
@@ -867,6 +853,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? R
     if (v.stats && lane == 0)  // state r/(w), root meta + children N, p row + idx, rng
         v.stats[(size_t)v.G + g] += ab + 32ull + (apply ? 32 : 0) + 12 +
                                     4ull * m_nchild(v.meta[(size_t)g * v.M]) + 8ull * NPOL + 4 + 16;
+    return idx;
+}
+
+#ifndef RVZ_ACT_WPE
+#define RVZ_ACT_WPE 6
+#endif
+// act: mcts.py:656-692 + self_play.py:98 (make_move of the sampled action); optionally preceded
+// by the last batch's pending expand + backup.
+template <int BS>
+// 8x8: <= 80 VGPRs (6 waves per SIMD), so a k_act wave fits on a SIMD beside two trunk waves
+// (2 x 216); the 6x6 form would spill under that cap
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BS == 8 ? RVZ_ACT_WPE : 1))) void k_act(View v, int expand, const float* __restrict__ policy,
+                                             int is_logits, const float* __restrict__ value,
+                                             double temperature, const double* __restrict__ uo,
+                                             int apply, int32_t* __restrict__ out_idx,
+                                             double* __restrict__ out_p) {
+    constexpr int NPOL = Geo<BS>::NPOL;
+    __shared__ double sp[WPB][NPOL + 7];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = blockIdx.x * WPB + wid;
+    if (g >= v.G) return;
+    // the search's leaf batches are all consumed (their NN calls precede this launch); the rows
+    // of a skipped last batch (expand == 2, rvz_search_skip) were handed out but not evaluated
+    if (v.live && lane == 0) {
+        const int counted = expand == 2 ? (v.E - 1) * v.NS : v.E * v.NS;
+        for (int i = g; i < v.E * v.NS; i += v.G) {
+            const int c = v.live[(size_t)i * RVZ_LIVE_PITCH];
+            if (c && i < counted) atomicAdd(v.live_total, (unsigned long long)c);
+            v.live[(size_t)i * RVZ_LIVE_PITCH] = 0;
+        }
+    }
+    act_game<BS>(v, g, lane, sp[wid], expand, policy, is_logits, value, temperature, uo, apply,
+                 out_idx, out_p);
 }
 
 // reset: new game (board.py:25-39) + np.random.seed(seed) random_sample() stream.
@@ -944,6 +963,8 @@ __global__ __launch_bounds__(256) void k_autoreset(View v, const int32_t* __rest
     sd = __shfl(sd, 0);
     reset_game<BS>(v, g, lane, (uint32_t)(sd & 0xFFFFFFFFll), key[wid]);
 }
+
+#include "rvz_play.hip.h"
 
 // ---- board kernels on caller arrays (one thread per board) --------------------------------------
 template <int BS>
@@ -1528,6 +1549,99 @@ int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, i
     e->live_dirty = 0;
     if (apply) e->searching = 0;
     return launch_check(e, "k_act");
+}
+
+static int64_t play_al4(int64_t n) { return (n + 3) / 4 * 4; }
+
+int64_t rvz_play_scratch_size(const rvz_engine* e) {
+    if (!e) return RVZ_EINVAL;
+    const int64_t G = e->v.G;
+    return play_al4(G * 3 * e->NSQ) + play_al4(G) + play_al4(G * 192) + play_al4(G * e->NPOL) +
+           play_al4(G);
+}
+
+extern "C++" {
+template <int F, int NB, int CTW, int PTW, int BS, int OCC>
+static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slots_per_cu) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->cfg.device) !=
+            hipSuccess || cus <= 0)
+        cus = 256;
+    PlayArgs a = pa;
+    if (a.gpw <= 0) {   // one workgroup per resident slot: every workgroup starts at once
+        const int slots = cus * slots_per_cu;
+        a.gpw = (v.G + slots - 1) / slots;
+    }
+    if (a.gpw > PLAY_GPW_MAX) a.gpw = PLAY_GPW_MAX;
+    const dim3 grid((v.G + a.gpw - 1) / a.gpw);
+    PlayCtx ctx;
+    ctx.v = v;
+    ctx.a = a;
+    hipLaunchKernelGGL((k_play<F, NB, CTW, PTW, BS, OCC>), grid, dim3(256), 0, e->stream, ctx);
+    return launch_check(e, "k_play");
+}
+}  // extern "C++"
+
+int rvz_play(rvz_engine* e, const rvz_play_args* a) {
+    const Range trace_range("rvz.play (fused search + h2 evaluator)");
+    if (!e || !a) return RVZ_EINVAL;
+    if (!a->params || !a->blob || !a->scratch || !a->seeds || !a->plies_done || !a->out_idx ||
+        !a->out_p || (a->reset && !a->games_done) || a->plies < 1 || a->blocks < 0 ||
+        (a->filters != 64 && a->filters != 128) || a->games_per_workgroup < 0 ||
+        e->cfg.leaf_dtype != RVZ_LEAF_F32) {
+        e->err = "rvz_play: invalid arguments";
+        return RVZ_EINVAL;
+    }
+    if ((((uintptr_t)a->params | (uintptr_t)a->blob | (uintptr_t)a->scratch) & 15) != 0) {
+        e->err = "rvz_play: params, blob and scratch must be 16-byte aligned";
+        return RVZ_EINVAL;
+    }
+    if (e->pending || (e->searching && e->next_batch > 0)) {
+        e->err = "rvz_play inside a search";
+        return RVZ_EINVAL;
+    }
+    View v = e->v;
+    v.live = nullptr;       // the workgroups compact their own rows
+    v.row_of = nullptr;
+    v.live_total = nullptr;
+    v.stats = nullptr;
+    const int64_t G = v.G;
+    PlayArgs pa;
+    pa.prm = a->params;
+    pa.L = make_layout(a->filters, a->blocks, e->BS);
+    pa.blob = a->blob;
+    pa.n_blocks = a->blocks;
+    float* sc = a->scratch;
+    pa.x = sc;
+    sc += play_al4(G * 3 * e->NSQ);
+    pa.need = reinterpret_cast<int32_t*>(sc);
+    sc += play_al4(G);
+    pa.work = sc;
+    sc += play_al4(G * 192);
+    pa.logits = sc;
+    sc += play_al4(G * e->NPOL);
+    pa.value = sc;
+    pa.ovf = a->ovf;
+    pa.gpw = a->games_per_workgroup;
+    pa.plies = a->plies;
+    pa.skip_last = a->skip_last_eval ? 1 : 0;
+    pa.reset = a->reset ? 1 : 0;
+    pa.S = e->cfg.num_simulations;
+    pa.B = e->cfg.batch_size;
+    pa.temperature = a->temperature;
+    pa.seeds = a->seeds;
+    pa.stride = a->seed_stride;
+    pa.ply_ctr = a->plies_done;
+    pa.done = a->games_done;
+    pa.out_idx = a->out_idx;
+    pa.out_p = a->out_p;
+    pa.hist = a->hist;
+    e->searching = 0;
+    if (e->BS == 8)
+        return a->filters == 64 ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)
+                                : play_launch<128, 1, 2, 4, 8, 2>(e, v, pa, 2);
+    return a->filters == 64 ? play_launch<64, 4, 2, 5, 6, 1>(e, v, pa, 1)
+                            : play_launch<128, 1, 2, 3, 6, 2>(e, v, pa, 2);
 }
 
 // ---- stream-ordered HIP event timer without system fence (bench.py: per-launch kernel

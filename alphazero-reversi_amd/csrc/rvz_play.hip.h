@@ -1,0 +1,220 @@
+// rvz_play.hip.h — fused self-play (rvz_play): a workgroup plays its own games, search and leaf
+// evaluation in one persistent launch. Included by csrc/rvz_engine.hip inside its anonymous
+// namespace, after the search device functions (select_phase, expand_backup_phase, act_game,
+// reset_game); the evaluator device functions come from rvz_h2.hip.h (h2_pass) and
+// rvz_resnet_common.hip.h (heads_fc16).
+//
+// The ply loop of SelfPlayRunner (per batch: k_step, the h2 trunk, the FC heads; then k_act and
+// k_autoreset, self_play.py:80-101 with mcts.py:322-407 and :642-694) as one launch:
+// workgroup w owns games [w * gpw, (w + 1) * gpw) and alternates
+//  * a search phase: one wave per game (four games at a time) runs the pending expand + the next
+//    batch's selection, or, after the last batch, act + autoreset, until the game has queued its
+//    next NN row or has committed `plies` plies in this launch;
+//  * an evaluation phase: the queued rows in NBOARD-board passes of the h2 trunk (h2_pass, the
+//    code of k_resnet_h2) and 16-board passes of the FC heads (heads_fc16, as k_heads_mfma).
+// Each per-game computation is the one the unfused launches make, and an h2 row's outputs depend
+// only on its position (test_h2_live_rows), so the games are bit-identical to SelfPlayRunner's
+// (tests/test_gpu_play.py). Inside a ply there is no kernel boundary, launch ramp or tail: the
+// two workgroups on a CU overlap one's search phase with the other's trunk passes.
+
+struct PlayArgs {
+    const float* prm;
+    Layout L;
+    const uint16_t* blob;
+    int n_blocks;
+    float* x;          // [G][3][NSQ] the queued rows' leaf planes (select_phase, row = game)
+    int32_t* need;     // [G] queued copies (select_phase)
+    float* work;       // [G][192] 1x1 head-conv outputs
+    float* logits;     // [G][NPOL]
+    float* value;      // [G]
+    float* ovf;        // sticky f16-overflow word of the evaluator, or null
+    int gpw, plies, skip_last, reset, S, B;
+    double temperature;
+    int64_t* seeds;
+    int64_t stride;
+    int64_t* ply_ctr;  // [G] committed plies per slot
+    int64_t* done;     // [G] finished games per slot
+    int32_t* out_idx;  // [G] the last act's index
+    double* out_p;     // [G][NPOL] the last act's policy vector
+    int32_t* hist;     // [plies][G] every act's index in this launch, or null
+};
+constexpr int PLAY_GPW_MAX = 64;
+enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4 };
+
+struct PlayCtx {
+    View v;
+    PlayArgs a;
+};
+// The launch's arguments, re-read from the kernarg segment at each use site: `play_ctx()` hides
+// the kernarg pointer from the optimiser (an empty asm), so the fields a phase reads are loaded
+// (s_load, scalar cache) inside that phase instead of being hoisted to the kernel entry and held
+// in SGPRs across the trunk passes (~100 SGPRs of View + PlayArgs: spills).
+// The thread index made opaque at the head of a phase: address arithmetic derived from it is
+// recomputed in that phase instead of being hoisted out of the ply loop and held in registers
+// across the other phases (the trunk, the search and the heads each need most of the registers)
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+__device__ __forceinline__ const PlayCtx& play_ctx() {
+    const __attribute__((address_space(4))) char* p =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const PlayCtx*)p;
+}
+
+template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
+void k_play(PlayCtx ctx0) {
+    (void)ctx0;   // read through play_ctx()
+    using WT = WaveTilesH<F, CTW, PTW>;
+    constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
+    using GH = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
+    using C = CfgH<F, GH::NPIX>;
+    constexpr int NPOL = Geo<BS>::NPOL;
+    // LDS: the trunk's activation image; between passes its head holds the search phase's act /
+    // reset scratch (per wave) or the FC heads' input rows
+    constexpr int SP_BYTES = WPB * (NPOL + 7) * 8;
+    static_assert(heads_in_floats(BS) * 4 <= C::BYTES, "heads rows fit");
+    static_assert(SP_BYTES + WPB * 624 * 4 <= C::BYTES, "act / reset scratch fits");
+    __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
+    __shared__ int st_k[PLAY_GPW_MAX];   // next batch of the game's search (E: act next)
+    __shared__ int st_f[PLAY_GPW_MAX];   // PF_* flags
+    __shared__ int st_p[PLAY_GPW_MAX];   // plies committed in this launch
+    __shared__ int q_rows[PLAY_GPW_MAX + 16];
+    __shared__ int s_nq;
+    __shared__ float vpart[4][16];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int g0, ng, E;
+    {
+        const PlayCtx& c = play_ctx();
+        g0 = blockIdx.x * c.a.gpw;
+        ng = min(c.a.gpw, c.v.G - g0);
+        E = c.v.E;
+    }
+    if (ng <= 0) return;
+    for (int j = tid; j < ng; j += 256) {
+        st_k[j] = 0;
+        st_f[j] = 0;
+        st_p[j] = 0;
+    }
+    __syncthreads();
+    bool ovf = false;
+    double* sp = reinterpret_cast<double*>(smem) + wave * (NPOL + 7);
+    uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
+    for (;;) {
+        // search phase: each game not waiting for its row advances until it queues the next
+        // row or has committed its plies (wave-uniform control flow per game)
+        for (int j = wave; j < ng; j += WPB) {
+            const PlayCtx& c = play_ctx();
+            const View& v = c.v;
+            const PlayArgs& a = c.a;
+            const int lane = opaque_tid() & 63;
+            const int g = g0 + j;
+            int f = __builtin_amdgcn_readfirstlane(st_f[j]);
+            if (f & (PF_QUEUED | PF_DONE)) continue;
+            int k = __builtin_amdgcn_readfirstlane(st_k[j]);
+            int np = __builtin_amdgcn_readfirstlane(st_p[j]);
+            for (;;) {
+                unsigned long long ab = 0;
+                if (k < E) {   // k_step: the pending expand + backup, then batch k's selection
+                    const int first = k == 0;
+                    const GameS root = load_game(v, g);
+                    uint32_t root_meta = 0, carry = LINK_NONE;
+                    int root_n = 0;
+                    if (!first) {
+                        root_meta = v.meta[(size_t)g * v.M];
+                        root_n = v.nodes[(size_t)g * v.M].n;
+                    } else if (v.memo) {
+                        carry = v.carry[g];
+                    }
+                    if (f & PF_READY) {
+                        const ExpIn x = expand_load<BS>(v, g, lane, a.logits, a.value);
+                        const int rn = expand_backup_phase<BS>(v, g, lane, x, 1, &root_meta, ab);
+                        if (rn >= 0) root_n = rn;
+                        f &= ~PF_READY;
+                    }
+                    const int bsz = min(a.B, a.S - k * a.B);
+                    const int copies = select_phase<BS, float>(v, g, lane, first, bsz, k, root,
+                                                               root_meta, root_n, carry, a.x,
+                                                               a.need, ab);
+                    ++k;
+                    // the last batch's row with skip_last: left unevaluated (rvz_search_skip)
+                    if (copies > 0 && !(k == E && a.skip_last)) {
+                        f |= PF_QUEUED;
+                        break;
+                    }
+                    continue;
+                }
+                // k_act: the last batch's expand (or visit-count backup), the action, the move
+                bool over = false;
+                const int idx = act_game<BS>(v, g, lane, sp, (f & PF_READY) ? 1 : 2, a.logits, 1,
+                                             a.value, a.temperature, nullptr, 1, a.out_idx,
+                                             a.out_p, &over);
+                f &= ~PF_READY;
+                // k_autoreset: count the ply; a finished game restarts with its slot's next seed
+                int64_t sd = 0;
+                if (lane == 0) {
+                    if (idx >= 0) a.ply_ctr[g] += 1;
+                    if (a.hist) a.hist[(size_t)np * v.G + g] = idx;
+                    if (a.reset && over) {
+                        a.done[g] += 1;
+                        sd = a.seeds[g] + a.stride;
+                        a.seeds[g] = sd;
+                    }
+                }
+                if (a.reset && over) {
+                    sd = __shfl(sd, 0);
+                    reset_game<BS>(v, g, lane, (uint32_t)(sd & 0xFFFFFFFFll), key);
+                }
+                ++np;
+                k = 0;
+                if (np >= a.plies) {
+                    f |= PF_DONE;
+                    break;
+                }
+            }
+            if (lane == 0) {
+                st_k[j] = k;
+                st_f[j] = f;
+                st_p[j] = np;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {   // the queued rows, in game order
+            int n = 0;
+            for (int j = 0; j < ng; ++j)
+                if (st_f[j] & PF_QUEUED) q_rows[n++] = g0 + j;
+            for (int i = n; i < n + 16; ++i) q_rows[i] = -1;
+            s_nq = n;
+        }
+        __syncthreads();
+        const int nq = __builtin_amdgcn_readfirstlane(s_nq);
+        if (nq == 0) break;   // every game has committed its plies
+
+        // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
+        for (int p0 = 0; p0 < nq; p0 += NBOARD) {
+            const PlayArgs& a = play_ctx().a;
+            int gb[NBOARD];
+#pragma unroll
+            for (int k = 0; k < NBOARD; ++k) gb[k] = q_rows[p0 + k];
+            const int t = opaque_tid();
+            h2_pass<F, NBOARD, CTW, PTW, BS>(smem, a.x, gb, a.prm, a.L, a.blob, a.n_blocks,
+                                             a.work, t, t & 63,
+                                             __builtin_amdgcn_readfirstlane(t >> 6), ovf);
+            __syncthreads();
+        }
+        for (int h0 = 0; h0 < nq; h0 += 16) {
+            const PlayArgs& a = play_ctx().a;
+            heads_fc16<BS>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
+                           reinterpret_cast<float*>(smem), vpart, opaque_tid());
+        }
+        for (int j = tid; j < ng; j += 256)
+            if (st_f[j] & PF_QUEUED) st_f[j] = (st_f[j] & ~PF_QUEUED) | PF_READY;
+        __syncthreads();
+    }
+    float* ovw = play_ctx().a.ovf;
+    if (ovf && ovw) *ovw = 1.0f;   // benign race: every writer stores 1
+}

@@ -147,23 +147,36 @@ __device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int
 #else
 #define RVZ_HEADS_ATTR
 #endif
-template <int BS>
-__global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
-    const float* __restrict__ work, int n, const float* __restrict__ prm, Layout L,
-    float* __restrict__ logits, float* __restrict__ value, const int32_t* __restrict__ n_live,
-    uint32_t* __restrict__ stamp_ctr) {
-    // bench.py: the trunk launch before this one is complete; advance its stamp ring
-    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
-    if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
+// Rows of the 16 board columns of one FC-heads pass: column b is row s0 + b (< n) of the
+// workspace / outputs (k_heads_mfma), or row rows[b] (>= 0; an LDS list: k_play)
+struct HeadRowsRange {
+    int s0, n;
+    __device__ int row(int b) const { return s0 + b < n ? s0 + b : -1; }
+};
+struct HeadRowsList {
+    const int* rows;   // [16], -1: no board
+    __device__ int row(int b) const { return rows[b]; }
+};
+__host__ __device__ constexpr int heads_in_floats(int BS) {
+    return 16 * ((2 * BS * BS + 15) / 16 * 16 + (BS * BS + 15) / 16 * 16 + 4);
+}
+// One pass of the FC heads over 16 board columns (the body of k_heads_mfma): `in` is
+// heads_in_floats(BS) floats of LDS, vpart 64; both free on entry. Ends with a barrier.
+template <int BS, class Rows>
+__device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const Rows& rmap,
+                                           const float* __restrict__ prm, const Layout& L,
+                                           float* __restrict__ logits, float* __restrict__ value,
+                                           float* __restrict__ in, float (*vpart)[16],
+                                           int tid = threadIdx.x) {
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
     constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
     constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
     constexpr int VJ = VK / 16, PJ = PK / 16, VTW = 256 / 16 / 4, PTW = (PT + 3) / 4;
     static_assert(CELLS % 4 == 0 && PIN % 4 == 0, "f32x4 rows");
-    __shared__ __attribute__((aligned(16))) float in[16 * ROW];
-    __shared__ float vpart[4][16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int g0 = blockIdx.x * 16, col = lane & 15, grp = lane >> 4;
+    static_assert(16 * ROW == heads_in_floats(BS), "LDS size");
+    const int lane = tid & 63, wave = tid >> 6;
+    const int col = lane & 15, grp = lane >> 4;
+    const int grow = rmap.row(col);                  // this lane's board column: its row
 #if RVZ_HEADS_STREAM
     // the wave's weight steps in order: value fc1 tiles wave + 4m (VJ steps each), then policy
     // tiles wave + 4m (PJ steps each); step s = one f32x4 of the A row (unit 16 t + col,
@@ -224,8 +237,9 @@ __global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
         for (int q = 0; q < NQ; ++q) {
             const int i = tid + 256 * q, b = i / RQ, k = 4 * (i % RQ);
             const int src = k < PIN ? k : (k >= PK && k - PK < CELLS ? PIN + k - PK : -1);
-            v[q] = g0 + b < n && src >= 0
-                       ? *reinterpret_cast<const f32x4*>(work + (size_t)(g0 + b) * 192 + src)
+            const int rb = rmap.row(b);
+            v[q] = rb >= 0 && src >= 0
+                       ? *reinterpret_cast<const f32x4*>(work + (size_t)rb * 192 + src)
                        : f32x4{};
         }
 #pragma unroll
@@ -272,11 +286,10 @@ __global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
         if (!val && j == PJ - 1 && t < PT) {
             const f32x4 pb = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                  rw, 16 * grp, (int)(L.pfc_b + 16 * t) * 4, 0));
-            const int g = g0 + col;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int oo = 16 * t + 4 * grp + r;
-                if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + pb[r];
+                if (oo < POUT && grow >= 0) logits[(size_t)grow * POUT + oo] = acc[r] + pb[r];
             }
         }
     }
@@ -290,11 +303,10 @@ __global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
         }
     };
     auto policy_tile = [&](int t, const f32x4& acc) {
-        const int g = g0 + col;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int oo = 16 * t + 4 * grp + r;
-            if (oo < POUT && g < n) logits[(size_t)g * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
+            if (oo < POUT && grow >= 0) logits[(size_t)grow * POUT + oo] = acc[r] + prm[L.pfc_b + oo];
         }
     };
     // value fc1 (+ bias, ReLU) and its fc2 partial
@@ -330,10 +342,28 @@ __global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
     }
 #endif
     __syncthreads();
-    if (tid < 16 && g0 + tid < n)
-        value[g0 + tid] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
-                                prm[L.vfc2_b]);
+    if (tid < 16) {
+        const int rt = rmap.row(tid);
+        if (rt >= 0)
+            value[rt] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
+                              prm[L.vfc2_b]);
+    }
+    __syncthreads();
 }
+
+template <int BS>
+__global__ __launch_bounds__(256) RVZ_HEADS_ATTR void k_heads_mfma(
+    const float* __restrict__ work, int n, const float* __restrict__ prm, Layout L,
+    float* __restrict__ logits, float* __restrict__ value, const int32_t* __restrict__ n_live,
+    uint32_t* __restrict__ stamp_ctr) {
+    // bench.py: the trunk launch before this one is complete; advance its stamp ring
+    if (stamp_ctr && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(stamp_ctr, 1u);
+    if (row_dead(n_live, (int)blockIdx.x * 16)) return;    // the workgroup's rows are all dead
+    __shared__ __attribute__((aligned(16))) float in[heads_in_floats(BS)];
+    __shared__ float vpart[4][16];
+    heads_fc16<BS>(work, HeadRowsRange{(int)blockIdx.x * 16, n}, prm, L, logits, value, in, vpart);
+}
+
 
 #ifdef RVZ_PHASE_TIMING   // tools/phase_timing.py: per-workgroup s_memtime at phase boundaries
 __device__ uint64_t g_phase[65536][8];

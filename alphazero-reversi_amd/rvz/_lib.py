@@ -72,6 +72,8 @@ SIGNATURES = {
     "rvz_search_skip": (C.c_int, [_P]),
     "rvz_search_visits": (C.c_int, [_P, _P]),
     "rvz_act": (C.c_int, [_P, C.c_double, _P, C.c_int32, _P, _P]),
+    "rvz_play_scratch_size": (C.c_int64, [_P]),
+    "rvz_play": (C.c_int, [_P, _P]),
     "rvz_counters": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "rvz_stats_enable": (C.c_int, [_P, C.c_int32]),
     "rvz_stats_read": (C.c_int, [_P, C.POINTER(C.c_int64)]),
@@ -93,6 +95,17 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+class PlayArgs(C.Structure):
+    """include/rvz.h rvz_play_args (pointers as integers: device addresses)."""
+    _fields_ = [("params", C.c_void_p), ("blob", C.c_void_p), ("filters", C.c_int32),
+                ("blocks", C.c_int32), ("scratch", C.c_void_p), ("ovf", C.c_void_p),
+                ("plies", C.c_int32), ("skip_last_eval", C.c_int32), ("reset", C.c_int32),
+                ("games_per_workgroup", C.c_int32), ("temperature", C.c_double),
+                ("seeds", C.c_void_p), ("seed_stride", C.c_int64), ("plies_done", C.c_void_p),
+                ("games_done", C.c_void_p), ("out_idx", C.c_void_p), ("out_p", C.c_void_p),
+                ("hist", C.c_void_p)]
 
 
 def load() -> C.CDLL:

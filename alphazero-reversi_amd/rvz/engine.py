@@ -210,6 +210,45 @@ class Engine:
         self._call("rvz_env_apply", ptr(s), ptr(ok))
         return ok
 
+    # ------------------------------------------------------------------ fused self-play
+    def play(self, evaluator, plies: int, temperature: float, seeds: torch.Tensor, stride: int,
+             plies_done: torch.Tensor, games_done: torch.Tensor, reset: bool = True,
+             skip_last_eval: bool = False, hist: Optional[torch.Tensor] = None,
+             games_per_workgroup: int = 0):
+        """rvz_play: every game commits `plies` plies (search of num_simulations + move + the
+        autoreset bookkeeping of autoreset()) in ONE launch, the h2 LeafEvaluator's trunk and
+        heads inside it; the same games, moves and counters as search() + act() + autoreset()
+        with that evaluator (fused_softmax). idx_buf / p_buf: each game's last act. hist: int32
+        [plies, n_games] for every act's index, or None. Graph-capturable."""
+        from .network import LeafEvaluator
+        if not isinstance(evaluator, LeafEvaluator):
+            raise RvzError("play() runs the h2 LeafEvaluator inside the launch; another "
+                           "evaluator goes through search() / act()")
+        if evaluator.board_size != self.board_size or evaluator.device != self.device:
+            raise RvzError("play(): the evaluator's board size / device differ from the engine's")
+        for t, dt in ((seeds, torch.int64), (plies_done, torch.int64), (games_done, torch.int64)):
+            if t.dtype != dt or t.numel() != self.n_games or not t.is_contiguous():
+                raise RvzError("play: seeds / plies_done / games_done int64 [n_games]")
+        if hist is not None and (hist.dtype != torch.int32 or hist.shape != (plies, self.n_games)
+                                 or not hist.is_contiguous()):
+            raise RvzError("play: hist int32 [plies, n_games]")
+        n = self.lib.rvz_play_scratch_size(self._h)
+        sc = getattr(self, "_play_scratch", None)
+        if sc is None or sc.numel() < n:
+            sc = torch.zeros(n, dtype=torch.float32, device=self.device)
+            self._play_scratch = sc
+        if evaluator not in getattr(self, "_evaluators", ()):
+            self._evaluators = tuple(getattr(self, "_evaluators", ())) + (evaluator,)
+        a = _lib.PlayArgs(evaluator.params.data_ptr(), evaluator.wsplit.data_ptr(),
+                          evaluator.filters, evaluator.n_blocks, sc.data_ptr(),
+                          evaluator.ovf_word().data_ptr(), int(plies), int(bool(skip_last_eval)),
+                          int(bool(reset)), int(games_per_workgroup), float(temperature),
+                          seeds.data_ptr(), int(stride), plies_done.data_ptr(),
+                          games_done.data_ptr(), self.idx_buf.data_ptr(), self.p_buf.data_ptr(),
+                          hist.data_ptr() if hist is not None else None)
+        self._stream()
+        self._call("rvz_play", C.byref(a))
+
     # ------------------------------------------------------------------ search
     def search_begin(self):
         self._call("rvz_search_begin")

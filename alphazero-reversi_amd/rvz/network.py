@@ -257,10 +257,19 @@ class LeafEvaluator:
 
     trunk_kernel_name = "k_resnet_h2"
 
+    def ovf_word(self) -> torch.Tensor:
+        """The sticky f16-overflow word the fused self-play launch (Engine.play) sets."""
+        w = getattr(self, "_ovf", None)
+        if w is None:
+            w = self._ovf = torch.zeros(4, device=self.device)
+        return w
+
     def overflowed(self) -> bool:
         """True if any activation of any call so far reached the f16 range limit
         (65520) — the outputs of that call are then not valid (synchronises)."""
-        return any(bool(w[-4].item() != 0) for _, _, w in self._outs.values())
+        fused = getattr(self, "_ovf", None)
+        return (any(bool(w[-4].item() != 0) for _, _, w in self._outs.values()) or
+                (fused is not None and bool(fused[0].item() != 0)))
 
     def mfma_flops_per_row(self) -> int:
         """FLOPs the trunk kernel executes on the f16 matrix cores per board: three partial

@@ -28,9 +28,15 @@ class SelfPlayRunner:
     def __init__(self, engine: Engine, evaluator: Callable, temperature: float = 1.0,
                  fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
                  record: bool = False, max_plies: int = 60, seed_stride: int = None,
-                 skip_last_eval: bool = False, fused_bookkeeping: bool = True):
+                 skip_last_eval: bool = False, fused_bookkeeping: bool = True,
+                 fused: bool = False):
         self.eng = engine
         self.skip_last_eval = bool(skip_last_eval)
+        # fused: each ply() is ONE rvz_play launch (Engine.play: search + the h2 evaluator +
+        # act + autoreset per workgroup) instead of the per-batch launches; same games
+        self.fused = bool(fused)
+        if self.fused and (record or not fused_softmax):
+            raise ValueError("the fused runner plays with fused_softmax and without records")
         # fused_bookkeeping: ply counting and autoreset in one engine kernel (rvz_env_autoreset)
         # instead of ~12 small torch kernels per ply; the games are the same either way
         self.fused_bookkeeping = bool(fused_bookkeeping)
@@ -80,8 +86,13 @@ class SelfPlayRunner:
         self.eng.check()
 
     # one ply for every game; graph-capturable (no host sync)
-    def _body(self):
+    def _body(self, plies: int = 1):
         eng = self.eng
+        if self.fused:
+            eng.play(self.evaluator, plies, self.temperature, self.seeds, self.seed_stride,
+                     self._plies, self._done, reset=self.autoreset,
+                     skip_last_eval=self.skip_last_eval)
+            return
         if self.record:          # the states before the move, for the game records
             b, w, st = eng.get_state()
             self.pre_black.copy_(b)
@@ -118,8 +129,11 @@ class SelfPlayRunner:
         torch.cuda.synchronize(self.eng.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(plies):
-                self._body()
+            if self.fused:
+                self._body(plies)          # one launch plays them all
+            else:
+                for _ in range(plies):
+                    self._body()
         self.graph = g
         self.plies_per_call = int(plies)
         torch.cuda.synchronize(self.eng.device)
@@ -127,6 +141,7 @@ class SelfPlayRunner:
     plies_per_call = 1        # plies one ply() call plays (a captured multi-ply graph: more)
 
     def ply(self):
+        """One ply of every game (a captured graph: plies_per_call plies)."""
         if self.graph is not None:
             self.graph.replay()
         else:
@@ -158,7 +173,7 @@ class LaneRunner:
     def __init__(self, make_engine: Callable[[int], Engine], make_evaluator: Callable,
                  n_games: int, lanes: int = 2, temperature: float = 1.0,
                  fused_softmax: bool = True, autoreset: bool = False, seed_base: int = 42,
-                 seed_stride: int = None, skip_last_eval: bool = False):
+                 seed_stride: int = None, skip_last_eval: bool = False, fused: bool = False):
         if lanes < 1 or n_games < lanes:
             raise ValueError("need 1 <= lanes <= n_games")
         sizes = [n_games // lanes + (1 if k < n_games % lanes else 0) for k in range(lanes)]
@@ -166,7 +181,8 @@ class LaneRunner:
         stride = n_games if seed_stride is None else int(seed_stride)
         self.runners = [SelfPlayRunner(make_engine(gl), make_evaluator(), temperature,
                                        fused_softmax, autoreset, seed_base + o,
-                                       seed_stride=stride, skip_last_eval=skip_last_eval)
+                                       seed_stride=stride, skip_last_eval=skip_last_eval,
+                                       fused=fused)
                         for gl, o in zip(sizes, offsets)]
         dev = self.runners[0].eng.device
         self.streams = [torch.cuda.Stream(dev) for _ in range(lanes)]
@@ -223,8 +239,11 @@ class LaneRunner:
             for r, s in zip(self.runners, self.streams):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, stream=s):
-                    for _ in range(plies):
-                        r._body()
+                    if r.fused:
+                        r._body(plies)
+                    else:
+                        for _ in range(plies):
+                            r._body()
                 self.lane_graphs.append(g)
         else:
             g = torch.cuda.CUDAGraph()

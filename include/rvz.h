@@ -158,6 +158,39 @@ int rvz_search_visits(rvz_engine *e, int32_t *out);
 int rvz_act(rvz_engine *e, double temperature, const double *u, int32_t apply, int32_t *out_idx,
             double *out_p);
 
+/* ---- fused self-play ---------------------------------------------------------------------
+ * Replaces SelfPlay.generate_games' ply loop (self_play.py:80-101: MCTS.search + get_action_probs
+ * + make_move, mcts.py:322-407 and :642-694) together with its leaf evaluator
+ * (AlphaZeroNetwork.predict, network.py:136-158) when the evaluator is the h2 ResNet: ONE launch in
+ * which each workgroup plays its own games, every game committing `plies` plies (each a full
+ * search of num_simulations), with the per-ply bookkeeping of rvz_env_autoreset. The games, moves,
+ * p and counters are bit-identical to the pull-style loop (rvz_search_step / the
+ * rvz_resnet_fwd_h2 evaluator with logits / rvz_search_submit / rvz_act / rvz_env_autoreset) on
+ * the same engine state; the engine's memo setting applies; compaction is inherent (only the live
+ * leaves are evaluated). Not inside a search; graph-capturable (no allocation, no sync). */
+typedef struct rvz_play_args {
+    const float *params;         /* packed fp32 net (rvz_resnet_params_size layout) */
+    const uint16_t *blob;        /* its h2 weight blob (rvz_resnet_h2_weights), 16-byte aligned */
+    int32_t filters;             /* 64 | 128 */
+    int32_t blocks;              /* residual blocks */
+    float *scratch;              /* rvz_play_scratch_size(e) floats, 16-byte aligned */
+    float *ovf;                  /* the evaluator's sticky f16-overflow word (set to 1), nullable */
+    int32_t plies;               /* plies every game commits in this call, >= 1 */
+    int32_t skip_last_eval;      /* each search's last batch unevaluated (rvz_search_skip) */
+    int32_t reset;               /* finished games restart (rvz_env_autoreset's reset) */
+    int32_t games_per_workgroup; /* 0: automatic (fill the device once) */
+    double temperature;
+    int64_t *seeds;              /* int64 [n_games], as rvz_env_autoreset */
+    int64_t seed_stride;
+    int64_t *plies_done;         /* int64 [n_games], += 1 per committed move */
+    int64_t *games_done;         /* int64 [n_games], += 1 per finished game (reset != 0) */
+    int32_t *out_idx;            /* int32 [n_games]: each game's last act (as rvz_act) */
+    double *out_p;               /* float64 [n_games, S*S+1]: its policy vector */
+    int32_t *hist;               /* int32 [plies][n_games]: every act's index, nullable */
+} rvz_play_args;
+int64_t rvz_play_scratch_size(const rvz_engine *e);
+int rvz_play(rvz_engine *e, const rvz_play_args *a);
+
 /* ---- introspection (tests / bench) -------------------------------------------------------- */
 /* Stream-ordered HIP event timer, events without system fence (the engine's own launch timing
  * uses the same): record i / j around launches on a stream, rvz_timer_elapsed synchronises on j

@@ -1,0 +1,120 @@
+"""The fused self-play launch (rvz_play / Engine.play / SelfPlayRunner(fused=True)): each
+workgroup plays its own games — search, h2 trunk + FC heads, act, autoreset — in one launch.
+Held bit for bit against the pull-style runner (per-batch k_step / trunk / heads launches, k_act,
+k_autoreset), which the other GPU tests pin to the oracle and the reference's recorded games:
+every ply's move of every game, the final boards, statuses, RNG-driven restarts and counters."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(board, blocks, filters, seed=0):
+    import rvz
+    torch.manual_seed(seed)
+    return rvz.AlphaZeroNetwork(board, blocks, filters).cuda().eval()
+
+
+def _plain(net, G, S, plies, memo, skip, seed_base=42):
+    import rvz
+    run = rvz.SelfPlayRunner(rvz.Engine(G, S, 64, board_size=net.board_size, compact_leaves=True,
+                                        memo=memo),
+                             rvz.LeafEvaluator(net), autoreset=True, seed_base=seed_base,
+                             skip_last_eval=skip)
+    run.start()
+    moves = []
+    for _ in range(plies):
+        run.ply()
+        moves.append(run.eng.idx_buf.clone())
+    return run, torch.stack(moves)
+
+
+def _fused(net, G, S, plies, memo, skip, seed_base=42, gpw=0, chunks=(None,)):
+    import rvz
+    eng = rvz.Engine(G, S, 64, board_size=net.board_size, memo=memo)
+    run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=seed_base,
+                             skip_last_eval=skip, fused=True)
+    run.start()
+    hs, done = [], 0
+    for c in chunks:              # plies per launch (None: all of them)
+        n = plies - done if c is None else c
+        hist = torch.full((n, G), -9, dtype=torch.int32, device="cuda")
+        eng.play(run.evaluator, n, 1.0, run.seeds, run.seed_stride, run._plies, run._done,
+                 reset=True, skip_last_eval=skip, hist=hist, games_per_workgroup=gpw)
+        hs.append(hist)
+        done += n
+    assert done == plies
+    return run, torch.cat(hs)
+
+
+def _same(a, b):
+    (ra, ma), (rb, mb) = a, b
+    assert ma.shape == mb.shape
+    for k in range(ma.shape[0]):
+        assert torch.equal(ma[k], mb[k]), f"ply {k}: {int((ma[k] != mb[k]).sum())} games differ"
+    for x, y in zip(ra.eng.get_state(), rb.eng.get_state()):
+        assert torch.equal(x, y)
+    assert torch.equal(ra._plies, rb._plies) and torch.equal(ra._done, rb._done)
+    assert torch.equal(ra.seeds, rb.seeds)
+    assert torch.equal(ra.eng.p_buf, rb.eng.p_buf)
+    ra.eng.check()
+    rb.eng.check()
+
+
+@pytest.mark.parametrize("memo,skip", [(False, False), (True, False), (True, True)])
+def test_fused_plays_the_runner_games(memo, skip):
+    """8x8, 6x64 net, 300 games x 200 sims over 70 plies (whole games and restarts)."""
+    net = _net(8, 6, 64)
+    G, S, plies = 300, 200, 70
+    _same(_fused(net, G, S, plies, memo, skip), _plain(net, G, S, plies, memo, skip))
+
+
+@pytest.mark.parametrize("gpw,chunks", [(1, (None,)), (3, (5, 1, 14)), (7, (20,)), (64, (20,))])
+def test_fused_workgroup_sizes_and_launch_splits(gpw, chunks):
+    """Games per workgroup 1 / 3 / 7 / 64 (a partial last workgroup, odd queues) and the plies
+    split over several launches: the same games."""
+    net = _net(8, 2, 64, seed=3)
+    G, S = 203, 128
+    _same(_fused(net, G, S, 20, True, True, gpw=gpw, chunks=chunks),
+          _plain(net, G, S, 20, True, True))
+
+
+@pytest.mark.parametrize("board,blocks,filters", [(8, 2, 128), (6, 2, 64), (6, 1, 128)])
+def test_fused_other_geometries(board, blocks, filters):
+    """The C3 trunk shape (128 filters, one board per pass) and the packed 6x6 geometry (C5)."""
+    net = _net(board, blocks, filters, seed=1)
+    G, S, plies = 160, 160 if board == 8 else 100, 24
+    _same(_fused(net, G, S, plies, True, True), _plain(net, G, S, plies, True, True))
+
+
+def test_fused_headline_configuration_at_full_size():
+    """bench.py's C2 workload at full size: 4,096 games x 800 sims, the 6x64 net, memo and the
+    last batch left to it, 64 plies (a whole game and its restarts): identical to the runner."""
+    net = _net(8, 6, 64)
+    G, S, plies = 4096, 800, 64
+    _same(_fused(net, G, S, plies, True, True), _plain(net, G, S, plies, True, True))
+
+
+def test_fused_graph_capture_and_errors():
+    """A captured fused ply replays the same games; play() refuses non-h2 evaluators and a
+    call inside a pull-style search."""
+    import rvz
+    net = _net(8, 1, 64)
+    G, S = 64, 96
+    eng = rvz.Engine(G, S, 64, memo=True)
+    run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=5, fused=True)
+    run.start()
+    run.ply()
+    run.capture(plies=3)
+    for _ in range(4):
+        run.ply()
+    ref, _ = _plain(net, G, S, 13, True, False, seed_base=5)
+    for x, y in zip(run.eng.get_state(), ref.eng.get_state()):
+        assert torch.equal(x, y)
+    assert torch.equal(run._plies, ref._plies)
+    with pytest.raises(rvz.RvzError):
+        eng.play(lambda x: net(x), 1, 1.0, run.seeds, G, run._plies, run._done)
+    eng.search_begin()
+    eng.search_step()
+    with pytest.raises(rvz.RvzError):
+        eng.play(run.evaluator, 1, 1.0, run.seeds, G, run._plies, run._done)

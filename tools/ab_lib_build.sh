@@ -6,10 +6,7 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/_ab
 while [ $# -ge 2 ]; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off \
-      -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt $2 -shared \
-      -o "tools/_ab/librvz_$1.so" alphazero-reversi_amd/csrc/rvz_engine.hip \
-      alphazero-reversi_amd/csrc/rvz_resnet.hip -ldl &
+  make -s -C alphazero-reversi_amd OUT="$PWD/tools/_ab/librvz_$1.so" BUILD="build/ab_$1" EXTRA="$2" &
   shift 2
 done
 wait
