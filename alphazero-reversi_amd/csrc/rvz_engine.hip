@@ -1225,7 +1225,7 @@ int rvz_check(rvz_engine* e, int32_t* host_err) {
         RVZ_HIP(hipMemsetAsync(e->v.err, 0, sizeof(int32_t), e->stream), e);
         e->err = "device error word " + std::to_string(h) +
                  " (1: rng stream exhausted, 2: node pool, 4: path depth, 8: non-finite NN "
-                 "value or probability)";
+                 "value or probability, 16: rvz_play queue wait timed out)";
         return RVZ_EDEVICE;
     }
     return RVZ_OK;
@@ -1553,13 +1553,19 @@ int rvz_act(rvz_engine* e, double temperature, const double* u, int32_t apply, i
 
 static int64_t play_al4(int64_t n) { return (n + 3) / 4 * 4; }
 
+// scratch (floats): [queue words: q_next + pad, q_done[G]] (one 16-B-aligned block at the start,
+// zeroed per launch), leaf planes, need, head-conv rows, logits, value
+static int64_t play_qwords(int64_t G) { return 4 + play_al4(G); }
 int64_t rvz_play_scratch_size(const rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
     const int64_t G = e->v.G;
-    return play_al4(G * 3 * e->NSQ) + play_al4(G) + play_al4(G * 192) + play_al4(G * e->NPOL) +
-           play_al4(G);
+    return play_qwords(G) + play_al4(G * 3 * e->NSQ) + play_al4(G) + play_al4(G * 192) +
+           play_al4(G * e->NPOL) + play_al4(G);
 }
 
+#ifndef RVZ_PLAY_GROUP
+#define RVZ_PLAY_GROUP 4      // games per task of the queue schedule
+#endif
 extern "C++" {
 template <int F, int NB, int CTW, int PTW, int BS, int OCC>
 static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slots_per_cu) {
@@ -1568,12 +1574,20 @@ static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slo
             hipSuccess || cus <= 0)
         cus = 256;
     PlayArgs a = pa;
-    if (a.gpw <= 0) {   // one workgroup per resident slot: every workgroup starts at once
-        const int slots = cus * slots_per_cu;
-        a.gpw = (v.G + slots - 1) / slots;
+    const int slots = cus * slots_per_cu;
+    dim3 grid;
+    if (a.q_next) {     // queue: one persistent workgroup per resident slot, groups of gpw games
+        if (a.gpw <= 0) a.gpw = RVZ_PLAY_GROUP;
+        if (a.gpw > PLAY_GPW_MAX) a.gpw = PLAY_GPW_MAX;
+        a.n_groups = (v.G + a.gpw - 1) / a.gpw;
+        grid = dim3(a.n_groups < slots ? a.n_groups : slots);
+        RVZ_HIP(hipMemsetAsync(a.q_next, 0, sizeof(float) * play_qwords(v.G), e->stream), e);
+    } else {            // static: workgroup w owns group w for every ply
+        if (a.gpw <= 0) a.gpw = (v.G + slots - 1) / slots;
+        if (a.gpw > PLAY_GPW_MAX) a.gpw = PLAY_GPW_MAX;
+        a.n_groups = (v.G + a.gpw - 1) / a.gpw;
+        grid = dim3(a.n_groups);
     }
-    if (a.gpw > PLAY_GPW_MAX) a.gpw = PLAY_GPW_MAX;
-    const dim3 grid((v.G + a.gpw - 1) / a.gpw);
     PlayCtx ctx;
     ctx.v = v;
     ctx.a = a;
@@ -1582,12 +1596,23 @@ static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slo
 }
 }  // extern "C++"
 
+#ifdef RVZ_PLAY_TIMING
+// tools/exp_play_phases.py: host copy of g_play_t (n workgroups x 8), then zeroed
+int rvz_play_timing_read(uint64_t* host, int n) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_play_t), (size_t)n * 8 * 8) != hipSuccess)
+        return RVZ_EHIP;
+    std::vector<unsigned long long> z((size_t)16384 * 8, 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_play_t), z.data(), z.size() * 8) == hipSuccess
+               ? RVZ_OK : RVZ_EHIP;
+}
+#endif
+
 int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     const Range trace_range("rvz.play (fused search + h2 evaluator)");
     if (!e || !a) return RVZ_EINVAL;
     if (!a->params || !a->blob || !a->scratch || !a->seeds || !a->plies_done || !a->out_idx ||
         !a->out_p || (a->reset && !a->games_done) || a->plies < 1 || a->blocks < 0 ||
-        (a->filters != 64 && a->filters != 128) || a->games_per_workgroup < 0 ||
+        (a->filters != 64 && a->filters != 128) || a->games_per_workgroup < -PLAY_GPW_MAX ||
         e->cfg.leaf_dtype != RVZ_LEAF_F32) {
         e->err = "rvz_play: invalid arguments";
         return RVZ_EINVAL;
@@ -1612,6 +1637,13 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.blob = a->blob;
     pa.n_blocks = a->blocks;
     float* sc = a->scratch;
+    // games_per_workgroup > 0: static groups of that size; <= 0: the task queue, groups of
+    // -games_per_workgroup games (0: RVZ_PLAY_GROUP)
+    const bool queue = a->games_per_workgroup <= 0;
+    pa.q_next = queue ? reinterpret_cast<unsigned*>(sc) : nullptr;
+    pa.q_done = queue ? reinterpret_cast<unsigned*>(sc) + 4 : nullptr;
+    pa.n_groups = 0;
+    sc += play_qwords(G);
     pa.x = sc;
     sc += play_al4(G * 3 * e->NSQ);
     pa.need = reinterpret_cast<int32_t*>(sc);
@@ -1622,7 +1654,7 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     sc += play_al4(G * e->NPOL);
     pa.value = sc;
     pa.ovf = a->ovf;
-    pa.gpw = a->games_per_workgroup;
+    pa.gpw = queue ? -a->games_per_workgroup : a->games_per_workgroup;
     pa.plies = a->plies;
     pa.skip_last = a->skip_last_eval ? 1 : 0;
     pa.reset = a->reset ? 1 : 0;
@@ -1636,6 +1668,7 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.out_idx = a->out_idx;
     pa.out_p = a->out_p;
     pa.hist = a->hist;
+    pa.rows = reinterpret_cast<unsigned long long*>(a->rows_evaluated);
     e->searching = 0;
     if (e->BS == 8)
         return a->filters == 64 ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)

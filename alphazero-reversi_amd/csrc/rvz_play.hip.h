@@ -37,9 +37,18 @@ struct PlayArgs {
     int32_t* out_idx;  // [G] the last act's index
     double* out_p;     // [G][NPOL] the last act's policy vector
     int32_t* hist;     // [plies][G] every act's index in this launch, or null
+    unsigned long long* rows;   // += the rows this launch evaluated, or null
+    // schedule. Static (q_next null): workgroup w owns game group w for all `plies` plies.
+    // Queue: tasks t = (group t % n_groups, ply t / n_groups) drawn in order from q_next; a
+    // group's ply p starts after q_done[group] reached p (its ply p-1 published: agent-scope
+    // release by the workgroup that played it, acquire by the next). Both zeroed per launch.
+    unsigned* q_next;
+    unsigned* q_done;  // [n_groups]
+    int n_groups;
 };
 constexpr int PLAY_GPW_MAX = 64;
 enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4 };
+constexpr int32_t ERR_SCHED = 16;   // a queue wait timed out (device error word)
 
 struct PlayCtx {
     View v;
@@ -64,6 +73,19 @@ __device__ __forceinline__ const PlayCtx& play_ctx() {
     return *(const PlayCtx*)p;
 }
 
+// RVZ_PLAY_TIMING (tools/exp_play_phases.py, instrumented builds only): per workgroup, shader
+// clocks (s_memtime) spent in [0] the search phase (to its barrier), [1] the trunk passes,
+// [2] the FC heads, [3] the whole launch; [4] cycles of the loop, [5] trunk passes, [6] rows,
+// [7] the workgroup's XCC / CU (HW_ID)
+#ifdef RVZ_PLAY_TIMING
+__device__ unsigned long long g_play_t[16384][8];
+#define PT_NOW(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
+#define PT_ADD(i, v) if (tid == 0 && blockIdx.x < 16384) g_play_t[blockIdx.x][i] += (v)
+#else
+#define PT_NOW(t)
+#define PT_ADD(i, v)
+#endif
+
 template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_play(PlayCtx ctx0) {
@@ -85,26 +107,74 @@ void k_play(PlayCtx ctx0) {
     __shared__ int q_rows[PLAY_GPW_MAX + 16];
     __shared__ int s_nq;
     __shared__ float vpart[4][16];
+    __shared__ int s_task[2];
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int g0, ng, E;
+    int E, G, gpw, total, queue, task_plies;
     {
         const PlayCtx& c = play_ctx();
-        g0 = blockIdx.x * c.a.gpw;
-        ng = min(c.a.gpw, c.v.G - g0);
         E = c.v.E;
+        G = c.v.G;
+        gpw = c.a.gpw;
+        queue = c.a.q_next != nullptr;
+        total = queue ? c.a.n_groups * c.a.plies : 0;
+        task_plies = queue ? 1 : c.a.plies;
     }
-    if (ng <= 0) return;
+    bool ovf = false;
+    int n_rows = 0;                      // rows this workgroup evaluated
+    double* sp = reinterpret_cast<double*>(smem) + wave * (NPOL + 7);
+    uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
+    PT_NOW(t_start);
+    for (int task_i = 0;; ++task_i) {
+    // ---- the next task: a game group and the ply it starts at
+    int gi, ply0;
+    if (!queue) {
+        if (task_i > 0) break;
+        gi = blockIdx.x;
+        ply0 = 0;
+    } else {
+        if (tid == 0) {
+            const PlayArgs& a = play_ctx().a;
+            const unsigned t = __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            int tg = -1, tp = 0;
+            if ((int)t < total) {
+                tg = (int)(t % (unsigned)a.n_groups);
+                tp = (int)(t / (unsigned)a.n_groups);
+                // the group's previous ply: played (and published) by the workgroup that drew it
+                // n_groups tasks ago, which is running; bounded spin
+                unsigned spins = 0;
+                while ((int)__hip_atomic_load(a.q_done + tg, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) < tp) {
+                    __builtin_amdgcn_s_sleep(4);
+                    if (++spins > (1u << 26)) {
+                        atomicOr(play_ctx().v.err, ERR_SCHED);
+                        tg = -1;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // ONE acquire after the match
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            s_task[0] = tg;
+            s_task[1] = tp;
+        }
+        __syncthreads();   // the other waves load the group's state after the acquire
+        gi = __builtin_amdgcn_readfirstlane(s_task[0]);
+        ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
+        if (gi < 0) break;
+    }
+    const int g0 = gi * gpw;
+    const int ng = min(gpw, G - g0);
+    if (ng <= 0) break;
     for (int j = tid; j < ng; j += 256) {
         st_k[j] = 0;
         st_f[j] = 0;
         st_p[j] = 0;
     }
     __syncthreads();
-    bool ovf = false;
-    double* sp = reinterpret_cast<double*>(smem) + wave * (NPOL + 7);
-    uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
     for (;;) {
+        PT_NOW(t_c0);
         // search phase: each game not waiting for its row advances until it queues the next
         // row or has committed its plies (wave-uniform control flow per game)
         for (int j = wave; j < ng; j += WPB) {
@@ -158,7 +228,7 @@ void k_play(PlayCtx ctx0) {
                 int64_t sd = 0;
                 if (lane == 0) {
                     if (idx >= 0) a.ply_ctr[g] += 1;
-                    if (a.hist) a.hist[(size_t)np * v.G + g] = idx;
+                    if (a.hist) a.hist[(size_t)(ply0 + np) * v.G + g] = idx;
                     if (a.reset && over) {
                         a.done[g] += 1;
                         sd = a.seeds[g] + a.stride;
@@ -171,7 +241,7 @@ void k_play(PlayCtx ctx0) {
                 }
                 ++np;
                 k = 0;
-                if (np >= a.plies) {
+                if (np >= task_plies) {
                     f |= PF_DONE;
                     break;
                 }
@@ -183,6 +253,9 @@ void k_play(PlayCtx ctx0) {
             }
         }
         __syncthreads();
+        PT_NOW(t_c1);
+        PT_ADD(0, t_c1 - t_c0);
+        PT_ADD(4, 1);
         if (tid == 0) {   // the queued rows, in game order
             int n = 0;
             for (int j = 0; j < ng; ++j)
@@ -193,6 +266,8 @@ void k_play(PlayCtx ctx0) {
         __syncthreads();
         const int nq = __builtin_amdgcn_readfirstlane(s_nq);
         if (nq == 0) break;   // every game has committed its plies
+        n_rows += nq;
+        PT_NOW(t_c2);
 
         // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
         for (int p0 = 0; p0 < nq; p0 += NBOARD) {
@@ -206,6 +281,10 @@ void k_play(PlayCtx ctx0) {
                                              __builtin_amdgcn_readfirstlane(t >> 6), ovf);
             __syncthreads();
         }
+        PT_NOW(t_c3);
+        PT_ADD(1, t_c3 - t_c2);
+        PT_ADD(5, (nq + NBOARD - 1) / NBOARD);
+        PT_ADD(6, nq);
         for (int h0 = 0; h0 < nq; h0 += 16) {
             const PlayArgs& a = play_ctx().a;
             heads_fc16<BS>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
@@ -214,7 +293,31 @@ void k_play(PlayCtx ctx0) {
         for (int j = tid; j < ng; j += 256)
             if (st_f[j] & PF_QUEUED) st_f[j] = (st_f[j] & ~PF_QUEUED) | PF_READY;
         __syncthreads();
+        PT_NOW(t_c4);
+        PT_ADD(2, t_c4 - t_c3);
     }
+    if (queue) {   // publish the group's ply: every wave drained, then ONE agent release + flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(play_ctx().a.q_done + gi, (unsigned)(ply0 + 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    }   // tasks
+#ifdef RVZ_PLAY_TIMING
+    {
+        PT_NOW(t_end);
+        PT_ADD(3, t_end - t_start);
+        if (tid == 0 && blockIdx.x < 16384)
+            g_play_t[blockIdx.x][7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                      __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
+#endif
     float* ovw = play_ctx().a.ovf;
     if (ovf && ovw) *ovw = 1.0f;   // benign race: every writer stores 1
+    unsigned long long* rows = play_ctx().a.rows;
+    if (rows && tid == 0) atomicAdd(rows, (unsigned long long)n_rows);
 }

@@ -105,7 +105,7 @@ class PlayArgs(C.Structure):
                 ("games_per_workgroup", C.c_int32), ("temperature", C.c_double),
                 ("seeds", C.c_void_p), ("seed_stride", C.c_int64), ("plies_done", C.c_void_p),
                 ("games_done", C.c_void_p), ("out_idx", C.c_void_p), ("out_p", C.c_void_p),
-                ("hist", C.c_void_p)]
+                ("hist", C.c_void_p), ("rows_evaluated", C.c_void_p)]
 
 
 def load() -> C.CDLL:

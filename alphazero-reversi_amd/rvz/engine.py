@@ -232,6 +232,8 @@ class Engine:
         if hist is not None and (hist.dtype != torch.int32 or hist.shape != (plies, self.n_games)
                                  or not hist.is_contiguous()):
             raise RvzError("play: hist int32 [plies, n_games]")
+        if getattr(self, "play_rows", None) is None:   # rows evaluated by play() calls
+            self.play_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
         n = self.lib.rvz_play_scratch_size(self._h)
         sc = getattr(self, "_play_scratch", None)
         if sc is None or sc.numel() < n:
@@ -245,7 +247,8 @@ class Engine:
                           int(bool(reset)), int(games_per_workgroup), float(temperature),
                           seeds.data_ptr(), int(stride), plies_done.data_ptr(),
                           games_done.data_ptr(), self.idx_buf.data_ptr(), self.p_buf.data_ptr(),
-                          hist.data_ptr() if hist is not None else None)
+                          hist.data_ptr() if hist is not None else None,
+                          self.play_rows.data_ptr())
         self._stream()
         self._call("rvz_play", C.byref(a))
 

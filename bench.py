@@ -104,6 +104,9 @@ def parse(argv=None):
     ap.add_argument("--plies-per-graph", type=int, default=1,
                     help="plies captured into each lane's HIP graph (one replay plays them all; "
                          "--steps must be a multiple)")
+    ap.add_argument("--fused", action="store_true",
+                    help="one rvz_play launch per ply: each workgroup plays its own games (search "
+                         "+ h2 evaluator + act + autoreset in one persistent kernel)")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="one graph for all lanes with a fork / join per ply (default: one "
                          "graph per lane on its own stream, no per-ply join; +0.9%% at C2)")
@@ -481,7 +484,17 @@ def selfplay(args, device, rank, world, full=True):
                           compact_leaves=not args.no_compact, memo=not args.no_memo)
 
     first_game = rank * args.games          # global game index space: rank r owns a shard
-    if args.lanes > 1:
+    if args.fused:
+        # one rvz_play launch per replay: every workgroup plays its own games (search + h2
+        # evaluator + act + autoreset); lanes are not needed (no per-batch launch chain)
+        args.lanes = 1
+        lane0 = run = rvz.SelfPlayRunner(make_eng(args.games), make_ev(), temperature=1.0,
+                                         fused_softmax=True, autoreset=True,
+                                         seed_base=args.seed + first_game,
+                                         seed_stride=args.games * world,
+                                         skip_last_eval=args.skip_last_eval, fused=True)
+        engines = [run.eng]
+    elif args.lanes > 1:
         run = rvz.LaneRunner(make_eng, make_ev, args.games, args.lanes, temperature=1.0,
                              fused_softmax=True, autoreset=True,
                              seed_base=args.seed + first_game, seed_stride=args.games * world,
@@ -511,7 +524,7 @@ def selfplay(args, device, rank, world, full=True):
     cap_kw["plies"] = ppg
     warm = max(args.warmup, 0 if args.no_graph else 1)
     for i in range(warm):
-        if i == 0 and not args.no_graph and not args.no_stamps:
+        if i == 0 and not args.no_graph and not args.no_stamps and not args.fused:
             run.ply()
             grid = _lib.load().rvz_resnet_h2_grid(args.board, args.filters, eng.n_games)
             ring = max(1, args.steps) * eng.n_batches
@@ -527,16 +540,30 @@ def selfplay(args, device, rank, world, full=True):
             run.capture(**cap_kw)
     torch.cuda.synchronize(device)
 
-    rows0 = sum(e.rows_total() for e in engines)
+    def rows_now():
+        if args.fused:
+            return sum(int(e.play_rows.item()) for e in engines)
+        return sum(e.rows_total() for e in engines)
+
+    rows0 = rows_now()
     if graph_events:
         graph_events[1].zero_()            # the ring starts with the timed region
     rdist.barrier()
     torch.cuda.synchronize(device)
     s0 = int(run.steps.item())
+    n_rep = args.steps // ppg
+    # fused: HIP events (no system fence) around every replay on its stream = the k_play
+    # launches' durations (a replay is one launch)
+    ftimer = _lib.Timer(2 * n_rep) if args.fused else None
+    fstream = _lib.stream_handle(device)
     t0 = time.perf_counter()
     t_enq = []
-    for _ in range(args.steps // ppg):     # one replay plays ppg plies
+    for i in range(n_rep):                 # one replay plays ppg plies
+        if ftimer is not None:
+            ftimer.record(fstream)
         run.ply()
+        if ftimer is not None:
+            ftimer.record(fstream)
         t_enq.append(time.perf_counter())
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
@@ -546,7 +573,7 @@ def selfplay(args, device, rank, world, full=True):
               f"device total {(t1 - t0) * 1e3:.1f} ms", file=sys.stderr)
     rdist.barrier()
     s1 = int(run.steps.item())
-    rows1 = sum(e.rows_total() for e in engines)
+    rows1 = rows_now()
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
@@ -580,7 +607,13 @@ def selfplay(args, device, rank, world, full=True):
            "useful_frac": round(upr * lane_games / (t_iso * 1e-3) / 1e12 / peak, 4),
            "timing": "HIP events over 10 back-to-back launches of one full batch, no other "
                      "lane running"}
-    if trunk_live:
+    if ftimer is not None:
+        durs = [ftimer.elapsed(2 * i, 2 * i + 1) for i in range(n_rep)]
+        t_tr, rows_tr = sum(durs) / n_rep, rows / n_rep
+        timing = (f"in the timed region: all {n_rep} k_play launches (one per graph replay, "
+                  f"{ppg} plies each), HIP events without system fence around each replay on "
+                  "its stream")
+    elif trunk_live:
         t_tr, rows_tr = trunk_live["ms"], trunk_live["rows"]
         timing = (f"in the timed region: all {trunk_live['launches']} trunk launches of lane 0, "
                   "first workgroup start to last end (device s_memrealtime stamps)")
@@ -590,10 +623,13 @@ def selfplay(args, device, rank, world, full=True):
     ach_u = upr * rows_tr / (t_tr * 1e-3) / 1e12
     region = fpr * rows / (t1 - t0) / 1e12      # every lane's evaluated rows / timed wall time
     traffic, traffic_src = (stored_traffic(args, "nn_trunk") if full else (None, None))
-    roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma",
+    roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma",
             "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4),
-            "flops": "executed 16-bit MFMA FLOPs (mfma_flops_per_row x rows_per_launch)",
+            "flops": "executed 16-bit MFMA FLOPs (mfma_flops_per_row x rows_per_launch)" +
+                     ("; k_play's MFMA work is its h2 trunk passes (the search, act and FC "
+                      "heads phases run in the same launch and count as time only)"
+                      if args.fused else ""),
             "mfma_flops_per_row": fpr,
             "useful_flops_per_row": upr,
             "useful_achieved": round(ach_u, 2), "useful_frac": round(ach_u / peak, 4),
@@ -739,7 +775,7 @@ def main_c4(args, rank, world, device):
     fl = ev.mfma_flops_per_row() * eng.n_games
     ach = fl / (t_tr * 1e-3) / 1e12
     uach = ev.useful_flops_per_row() * eng.n_games / (t_tr * 1e-3) / 1e12
-    roof = {"kernel": ev.trunk_kernel_name, "bound": "mfma", "achieved": round(ach, 2),
+    roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma", "achieved": round(ach, 2),
             "peak": MFMA16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / MFMA16_PEAK_TFLOPS, 4),
             "mfma_flops_per_row": ev.mfma_flops_per_row(),
@@ -848,7 +884,10 @@ def main():
                                    f"{args.blocks}x{args.filters} ResNet, {args.board}x{args.board}",
                        "games_per_gpu": args.games, "global_games": args.games * world,
                        "sims": args.sims, "batch": args.batch,
-                       "nn": f"{args.blocks}x{args.filters}", "nn_kernel": "rvz_resnet_fwd_h2",
+                       "nn": f"{args.blocks}x{args.filters}",
+                       "nn_kernel": ("k_play (h2_pass + heads_fc16 inside the fused self-play "
+                                     "launch)" if args.fused else "rvz_resnet_fwd_h2"),
+                       "fused": args.fused, "plies_per_graph": args.plies_per_graph,
                        "graph": not args.no_graph, "lanes": args.lanes,
                        "lane_graphs": ("joined" if args.joined_lanes else "free")
                        if args.lanes > 1 else None,

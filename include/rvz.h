@@ -178,7 +178,9 @@ typedef struct rvz_play_args {
     int32_t plies;               /* plies every game commits in this call, >= 1 */
     int32_t skip_last_eval;      /* each search's last batch unevaluated (rvz_search_skip) */
     int32_t reset;               /* finished games restart (rvz_env_autoreset's reset) */
-    int32_t games_per_workgroup; /* 0: automatic (fill the device once) */
+    int32_t games_per_workgroup; /* > 0: static schedule, each workgroup owns that many games for
+                                    every ply; <= 0: task queue, the workgroups draw (group of
+                                    -games_per_workgroup games, ply) tasks (0: 4 games) */
     double temperature;
     int64_t *seeds;              /* int64 [n_games], as rvz_env_autoreset */
     int64_t seed_stride;
@@ -187,6 +189,7 @@ typedef struct rvz_play_args {
     int32_t *out_idx;            /* int32 [n_games]: each game's last act (as rvz_act) */
     double *out_p;               /* float64 [n_games, S*S+1]: its policy vector */
     int32_t *hist;               /* int32 [plies][n_games]: every act's index, nullable */
+    int64_t *rows_evaluated;     /* int64 [1] += the leaf rows evaluated by the call, nullable */
 } rvz_play_args;
 int64_t rvz_play_scratch_size(const rvz_engine *e);
 int rvz_play(rvz_engine *e, const rvz_play_args *a);
