@@ -126,194 +126,198 @@ void k_play(PlayCtx ctx0) {
     uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
     PT_NOW(t_start);
     for (int task_i = 0;; ++task_i) {
-    // ---- the next task: a game group and the ply it starts at
-    int gi, ply0;
-    if (!queue) {
-        if (task_i > 0) break;
-        gi = blockIdx.x;
-        ply0 = 0;
-    } else {
-        if (tid == 0) {
-            const PlayArgs& a = play_ctx().a;
-            const unsigned t = __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-            int tg = -1, tp = 0;
-            if ((int)t < total) {
-                tg = (int)(t % (unsigned)a.n_groups);
-                tp = (int)(t / (unsigned)a.n_groups);
-                // the group's previous ply: played (and published) by the workgroup that drew it
-                // n_groups tasks ago, which is running; bounded spin
-                unsigned spins = 0;
-                while ((int)__hip_atomic_load(a.q_done + tg, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) < tp) {
-                    __builtin_amdgcn_s_sleep(4);
-                    if (++spins > (1u << 26)) {
-                        atomicOr(play_ctx().v.err, ERR_SCHED);
-                        tg = -1;
-                        break;
+        // ---- the next task: a game group and the ply it starts at
+        int gi, ply0;
+        if (!queue) {
+            if (task_i > 0) break;
+            gi = blockIdx.x;
+            ply0 = 0;
+        } else {
+            if (tid == 0) {
+                const PlayArgs& a = play_ctx().a;
+                const unsigned t = __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                int tg = -1, tp = 0;
+                if ((int)t < total) {
+                    tg = (int)(t % (unsigned)a.n_groups);
+                    tp = (int)(t / (unsigned)a.n_groups);
+                    // the group's previous ply: played (and published) by the workgroup that
+                    // drew it n_groups tasks ago, which is running; bounded spin
+                    unsigned spins = 0;
+                    while ((int)__hip_atomic_load(a.q_done + tg, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT) < tp) {
+                        __builtin_amdgcn_s_sleep(4);
+                        if (++spins > (1u << 26)) {
+                            atomicOr(play_ctx().v.err, ERR_SCHED);
+                            tg = -1;
+                            break;
+                        }
                     }
+                    // ONE acquire after the match
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // ONE acquire after the match
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                s_task[0] = tg;
+                s_task[1] = tp;
             }
-            s_task[0] = tg;
-            s_task[1] = tp;
+            __syncthreads();   // the other waves load the group's state after the acquire
+            gi = __builtin_amdgcn_readfirstlane(s_task[0]);
+            ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
+            if (gi < 0) break;
         }
-        __syncthreads();   // the other waves load the group's state after the acquire
-        gi = __builtin_amdgcn_readfirstlane(s_task[0]);
-        ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
-        if (gi < 0) break;
-    }
-    const int g0 = gi * gpw;
-    const int ng = min(gpw, G - g0);
-    if (ng <= 0) break;
-    for (int j = tid; j < ng; j += 256) {
-        st_k[j] = 0;
-        st_f[j] = 0;
-        st_p[j] = 0;
-    }
-    __syncthreads();
-    for (;;) {
-        PT_NOW(t_c0);
-        // search phase: each game not waiting for its row advances until it queues the next
-        // row or has committed its plies (wave-uniform control flow per game)
-        for (int j = wave; j < ng; j += WPB) {
-            const PlayCtx& c = play_ctx();
-            const View& v = c.v;
-            const PlayArgs& a = c.a;
-            const int lane = opaque_tid() & 63;
-            const int g = g0 + j;
-            int f = __builtin_amdgcn_readfirstlane(st_f[j]);
-            if (f & (PF_QUEUED | PF_DONE)) continue;
-            int k = __builtin_amdgcn_readfirstlane(st_k[j]);
-            int np = __builtin_amdgcn_readfirstlane(st_p[j]);
-            for (;;) {
-                unsigned long long ab = 0;
-                if (k < E) {   // k_step: the pending expand + backup, then batch k's selection
-                    const int first = k == 0;
-                    const GameS root = load_game(v, g);
-                    uint32_t root_meta = 0, carry = LINK_NONE;
-                    int root_n = 0;
-                    if (!first) {
-                        root_meta = v.meta[(size_t)g * v.M];
-                        root_n = v.nodes[(size_t)g * v.M].n;
-                    } else if (v.memo) {
-                        carry = v.carry[g];
+        const int g0 = gi * gpw;
+        const int ng = min(gpw, G - g0);
+        if (ng <= 0) break;
+        for (int j = tid; j < ng; j += 256) {
+            st_k[j] = 0;
+            st_f[j] = 0;
+            st_p[j] = 0;
+        }
+        __syncthreads();
+        for (;;) {
+            PT_NOW(t_c0);
+            // search phase: each game not waiting for its row advances until it queues the next
+            // row or has committed its plies (wave-uniform control flow per game)
+            for (int j = wave; j < ng; j += WPB) {
+                const PlayCtx& c = play_ctx();
+                const View& v = c.v;
+                const PlayArgs& a = c.a;
+                const int lane = opaque_tid() & 63;
+                const int g = g0 + j;
+                int f = __builtin_amdgcn_readfirstlane(st_f[j]);
+                if (f & (PF_QUEUED | PF_DONE)) continue;
+                int k = __builtin_amdgcn_readfirstlane(st_k[j]);
+                int np = __builtin_amdgcn_readfirstlane(st_p[j]);
+                for (;;) {
+                    unsigned long long ab = 0;
+                    if (k < E) {   // k_step: the pending expand + backup, then batch k's selection
+                        const int first = k == 0;
+                        const GameS root = load_game(v, g);
+                        uint32_t root_meta = 0, carry = LINK_NONE;
+                        int root_n = 0;
+                        if (!first) {
+                            root_meta = v.meta[(size_t)g * v.M];
+                            root_n = v.nodes[(size_t)g * v.M].n;
+                        } else if (v.memo) {
+                            carry = v.carry[g];
+                        }
+                        if (f & PF_READY) {
+                            const ExpIn x = expand_load<BS>(v, g, lane, a.logits, a.value);
+                            const int rn =
+                                expand_backup_phase<BS>(v, g, lane, x, 1, &root_meta, ab);
+                            if (rn >= 0) root_n = rn;
+                            f &= ~PF_READY;
+                        }
+                        const int bsz = min(a.B, a.S - k * a.B);
+                        const int copies = select_phase<BS, float>(v, g, lane, first, bsz, k, root,
+                                                                   root_meta, root_n, carry, a.x,
+                                                                   a.need, ab);
+                        ++k;
+                        // the last batch's row with skip_last: left unevaluated (rvz_search_skip)
+                        if (copies > 0 && !(k == E && a.skip_last)) {
+                            f |= PF_QUEUED;
+                            break;
+                        }
+                        continue;
                     }
-                    if (f & PF_READY) {
-                        const ExpIn x = expand_load<BS>(v, g, lane, a.logits, a.value);
-                        const int rn = expand_backup_phase<BS>(v, g, lane, x, 1, &root_meta, ab);
-                        if (rn >= 0) root_n = rn;
-                        f &= ~PF_READY;
+                    // k_act: the last batch's expand (or visit-count backup), the action, the move
+                    bool over = false;
+                    const int idx = act_game<BS>(v, g, lane, sp, (f & PF_READY) ? 1 : 2,
+                                                 a.logits, 1, a.value, a.temperature, nullptr, 1,
+                                                 a.out_idx, a.out_p, &over);
+                    f &= ~PF_READY;
+                    // k_autoreset: count the ply; a finished game restarts with its slot's next
+                    // seed
+                    int64_t sd = 0;
+                    if (lane == 0) {
+                        if (idx >= 0) a.ply_ctr[g] += 1;
+                        if (a.hist) a.hist[(size_t)(ply0 + np) * v.G + g] = idx;
+                        if (a.reset && over) {
+                            a.done[g] += 1;
+                            sd = a.seeds[g] + a.stride;
+                            a.seeds[g] = sd;
+                        }
                     }
-                    const int bsz = min(a.B, a.S - k * a.B);
-                    const int copies = select_phase<BS, float>(v, g, lane, first, bsz, k, root,
-                                                               root_meta, root_n, carry, a.x,
-                                                               a.need, ab);
-                    ++k;
-                    // the last batch's row with skip_last: left unevaluated (rvz_search_skip)
-                    if (copies > 0 && !(k == E && a.skip_last)) {
-                        f |= PF_QUEUED;
-                        break;
-                    }
-                    continue;
-                }
-                // k_act: the last batch's expand (or visit-count backup), the action, the move
-                bool over = false;
-                const int idx = act_game<BS>(v, g, lane, sp, (f & PF_READY) ? 1 : 2, a.logits, 1,
-                                             a.value, a.temperature, nullptr, 1, a.out_idx,
-                                             a.out_p, &over);
-                f &= ~PF_READY;
-                // k_autoreset: count the ply; a finished game restarts with its slot's next seed
-                int64_t sd = 0;
-                if (lane == 0) {
-                    if (idx >= 0) a.ply_ctr[g] += 1;
-                    if (a.hist) a.hist[(size_t)(ply0 + np) * v.G + g] = idx;
                     if (a.reset && over) {
-                        a.done[g] += 1;
-                        sd = a.seeds[g] + a.stride;
-                        a.seeds[g] = sd;
+                        sd = __shfl(sd, 0);
+                        reset_game<BS>(v, g, lane, (uint32_t)(sd & 0xFFFFFFFFll), key);
+                    }
+                    ++np;
+                    k = 0;
+                    if (np >= task_plies) {
+                        f |= PF_DONE;
+                        break;
                     }
                 }
-                if (a.reset && over) {
-                    sd = __shfl(sd, 0);
-                    reset_game<BS>(v, g, lane, (uint32_t)(sd & 0xFFFFFFFFll), key);
-                }
-                ++np;
-                k = 0;
-                if (np >= task_plies) {
-                    f |= PF_DONE;
-                    break;
+                if (lane == 0) {
+                    st_k[j] = k;
+                    st_f[j] = f;
+                    st_p[j] = np;
                 }
             }
-            if (lane == 0) {
-                st_k[j] = k;
-                st_f[j] = f;
-                st_p[j] = np;
-            }
-        }
-        __syncthreads();
-        PT_NOW(t_c1);
-        PT_ADD(0, t_c1 - t_c0);
-        PT_ADD(4, 1);
-        if (tid == 0) {   // the queued rows, in game order
-            int n = 0;
-            for (int j = 0; j < ng; ++j)
-                if (st_f[j] & PF_QUEUED) q_rows[n++] = g0 + j;
-            for (int i = n; i < n + 16; ++i) q_rows[i] = -1;
-            s_nq = n;
-        }
-        __syncthreads();
-        const int nq = __builtin_amdgcn_readfirstlane(s_nq);
-        if (nq == 0) break;   // every game has committed its plies
-        n_rows += nq;
-        PT_NOW(t_c2);
-
-        // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
-        for (int p0 = 0; p0 < nq; p0 += NBOARD) {
-            const PlayArgs& a = play_ctx().a;
-            int gb[NBOARD];
-#pragma unroll
-            for (int k = 0; k < NBOARD; ++k) gb[k] = q_rows[p0 + k];
-            const int t = opaque_tid();
-            h2_pass<F, NBOARD, CTW, PTW, BS>(smem, a.x, gb, a.prm, a.L, a.blob, a.n_blocks,
-                                             a.work, t, t & 63,
-                                             __builtin_amdgcn_readfirstlane(t >> 6), ovf);
             __syncthreads();
+            PT_NOW(t_c1);
+            PT_ADD(0, t_c1 - t_c0);
+            PT_ADD(4, 1);
+            if (tid == 0) {   // the queued rows, in game order
+                int n = 0;
+                for (int j = 0; j < ng; ++j)
+                    if (st_f[j] & PF_QUEUED) q_rows[n++] = g0 + j;
+                for (int i = n; i < n + 16; ++i) q_rows[i] = -1;
+                s_nq = n;
+            }
+            __syncthreads();
+            const int nq = __builtin_amdgcn_readfirstlane(s_nq);
+            if (nq == 0) break;   // every game has committed its plies
+            n_rows += nq;
+            PT_NOW(t_c2);
+
+            // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
+            for (int p0 = 0; p0 < nq; p0 += NBOARD) {
+                const PlayArgs& a = play_ctx().a;
+                int gb[NBOARD];
+#pragma unroll
+                for (int k = 0; k < NBOARD; ++k) gb[k] = q_rows[p0 + k];
+                const int t = opaque_tid();
+                h2_pass<F, NBOARD, CTW, PTW, BS>(smem, a.x, gb, a.prm, a.L, a.blob, a.n_blocks,
+                                                 a.work, t, t & 63,
+                                                 __builtin_amdgcn_readfirstlane(t >> 6), ovf);
+                __syncthreads();
+            }
+            PT_NOW(t_c3);
+            PT_ADD(1, t_c3 - t_c2);
+            PT_ADD(5, (nq + NBOARD - 1) / NBOARD);
+            PT_ADD(6, nq);
+            for (int h0 = 0; h0 < nq; h0 += 16) {
+                const PlayArgs& a = play_ctx().a;
+                heads_fc16<BS>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
+                               reinterpret_cast<float*>(smem), vpart, opaque_tid());
+            }
+            for (int j = tid; j < ng; j += 256)
+                if (st_f[j] & PF_QUEUED) st_f[j] = (st_f[j] & ~PF_QUEUED) | PF_READY;
+            __syncthreads();
+            PT_NOW(t_c4);
+            PT_ADD(2, t_c4 - t_c3);
         }
-        PT_NOW(t_c3);
-        PT_ADD(1, t_c3 - t_c2);
-        PT_ADD(5, (nq + NBOARD - 1) / NBOARD);
-        PT_ADD(6, nq);
-        for (int h0 = 0; h0 < nq; h0 += 16) {
-            const PlayArgs& a = play_ctx().a;
-            heads_fc16<BS>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
-                           reinterpret_cast<float*>(smem), vpart, opaque_tid());
-        }
-        for (int j = tid; j < ng; j += 256)
-            if (st_f[j] & PF_QUEUED) st_f[j] = (st_f[j] & ~PF_QUEUED) | PF_READY;
-        __syncthreads();
-        PT_NOW(t_c4);
-        PT_ADD(2, t_c4 - t_c3);
-    }
-    if (queue) {   // publish the group's ply: every wave drained, then ONE agent release + flag
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (queue) {   // publish the group's ply: every wave drained, then ONE agent release + flag
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(play_ctx().a.q_done + gi, (unsigned)(ply0 + 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            __syncthreads();
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(play_ctx().a.q_done + gi, (unsigned)(ply0 + 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
-    }   // tasks
 #ifdef RVZ_PLAY_TIMING
     {
         PT_NOW(t_end);
         PT_ADD(3, t_end - t_start);
         if (tid == 0 && blockIdx.x < 16384)
-            g_play_t[blockIdx.x][7] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
-                                      __builtin_amdgcn_s_getreg((31 << 11) | 4);
+            g_play_t[blockIdx.x][7] =
+                ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                __builtin_amdgcn_s_getreg((31 << 11) | 4);
     }
 #endif
     float* ovw = play_ctx().a.ovf;
