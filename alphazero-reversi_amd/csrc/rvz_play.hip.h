@@ -290,7 +290,8 @@ void k_play(PlayCtx ctx0) {
             PT_ADD(6, nq);
             for (int h0 = 0; h0 < nq; h0 += 16) {
                 const PlayArgs& a = play_ctx().a;
-                heads_fc16<BS>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
+                heads_fc16<BS, HeadRowsList, false>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L,
+                                                a.logits, a.value,
                                reinterpret_cast<float*>(smem), vpart, opaque_tid());
             }
             for (int j = tid; j < ng; j += 256)

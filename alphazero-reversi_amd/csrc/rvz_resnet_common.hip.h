@@ -162,7 +162,10 @@ __host__ __device__ constexpr int heads_in_floats(int BS) {
 }
 // One pass of the FC heads over 16 board columns (the body of k_heads_mfma): `in` is
 // heads_in_floats(BS) floats of LDS, vpart 64; both free on entry. Ends with a barrier.
-template <int BS, class Rows>
+// STREAM: the weight fragments streamed RVZ_HEADS_PD steps ahead (76 VGPRs: k_heads_mfma's
+// waves fit beside two trunk waves), or all issued up front (one L2 round trip; ~148 VGPRs: the
+// fused k_play, whose register budget is the trunk's)
+template <int BS, class Rows, bool STREAM = RVZ_HEADS_STREAM != 0>
 __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const Rows& rmap,
                                            const float* __restrict__ prm, const Layout& L,
                                            float* __restrict__ logits, float* __restrict__ value,
@@ -177,7 +180,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
     const int lane = tid & 63, wave = tid >> 6;
     const int col = lane & 15, grp = lane >> 4;
     const int grow = rmap.row(col);                  // this lane's board column: its row
-#if RVZ_HEADS_STREAM
+
     // the wave's weight steps in order: value fc1 tiles wave + 4m (VJ steps each), then policy
     // tiles wave + 4m (PJ steps each); step s = one f32x4 of the A row (unit 16 t + col,
     // k = 16 j + 4 grp .. +3)
@@ -204,12 +207,15 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
                    : f32x4{};
     };
     f32x4 wq[D];
+    if constexpr (STREAM) {
 #pragma unroll
-    for (int s = 0; s < D; ++s) wq[s] = load_step(s);
-#else
+        for (int s = 0; s < D; ++s) wq[s] = load_step(s);
+    }
+
     // every weight fragment of this wave's tiles, issued before anything waits: value fc1 tiles
     // wave + 4m, policy tiles wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
     f32x4 av[VTW][VJ], ap[PTW][PJ];
+    if constexpr (!STREAM) {
 #pragma unroll
     for (int m = 0; m < VTW; ++m) {
         const float* wr = prm + L.vfc1_w + (size_t)(16 * (wave + 4 * m) + col) * CELLS + 4 * grp;
@@ -227,7 +233,8 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
             ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
                            ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
     }
-#endif
+    }
+
     {   // the 16 workspace rows into LDS, 16 B per load, all loads in flight before the stores
         // (policy planes at k < PIN, the value plane at PK.., zeros between)
         constexpr int RQ = (PK + VK) / 4, NQ = 16 * RQ / 256;
@@ -251,7 +258,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
     __syncthreads();
     const float* inb = in + col * ROW + 4 * grp;
     float vp = 0.0f;
-#if RVZ_HEADS_STREAM
+    if constexpr (STREAM) {
     f32x4 acc = {};
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
@@ -293,7 +300,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
             }
         }
     }
-#else
+    } else {
     // value fc1 tile epilogue (+ bias, ReLU) into the fc2 partial
     auto value_tile = [&](int m, const f32x4& acc) {
 #pragma unroll
@@ -340,7 +347,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
         }
         policy_tile(t, acc);
     }
-#endif
+    }
     __syncthreads();
     if (tid < 16) {
         const int rt = rmap.row(tid);

@@ -35,6 +35,7 @@ class SelfPlayRunner:
         # fused: each ply() is ONE rvz_play launch (Engine.play: search + the h2 evaluator +
         # act + autoreset per workgroup) instead of the per-batch launches; same games
         self.fused = bool(fused)
+        self.play_group = 0       # Engine.play's games_per_workgroup (0: the task queue default)
         if self.fused and (record or not fused_softmax):
             raise ValueError("the fused runner plays with fused_softmax and without records")
         # fused_bookkeeping: ply counting and autoreset in one engine kernel (rvz_env_autoreset)
@@ -91,7 +92,8 @@ class SelfPlayRunner:
         if self.fused:
             eng.play(self.evaluator, plies, self.temperature, self.seeds, self.seed_stride,
                      self._plies, self._done, reset=self.autoreset,
-                     skip_last_eval=self.skip_last_eval)
+                     skip_last_eval=self.skip_last_eval,
+                     games_per_workgroup=self.play_group)
             return
         if self.record:          # the states before the move, for the game records
             b, w, st = eng.get_state()

@@ -107,6 +107,9 @@ def parse(argv=None):
     ap.add_argument("--fused", action="store_true",
                     help="one rvz_play launch per ply: each workgroup plays its own games (search "
                          "+ h2 evaluator + act + autoreset in one persistent kernel)")
+    ap.add_argument("--play-group", type=int, default=0,
+                    help="--fused: rvz_play games_per_workgroup (> 0 static ownership; <= 0 the "
+                         "task queue with groups of -N games, 0 the default)")
     ap.add_argument("--joined-lanes", action="store_true",
                     help="one graph for all lanes with a fork / join per ply (default: one "
                          "graph per lane on its own stream, no per-ply join; +0.9%% at C2)")
@@ -493,6 +496,7 @@ def selfplay(args, device, rank, world, full=True):
                                          seed_base=args.seed + first_game,
                                          seed_stride=args.games * world,
                                          skip_last_eval=args.skip_last_eval, fused=True)
+        run.play_group = args.play_group
         engines = [run.eng]
     elif args.lanes > 1:
         run = rvz.LaneRunner(make_eng, make_ev, args.games, args.lanes, temperature=1.0,
