@@ -47,7 +47,9 @@ struct PlayArgs {
     int n_groups;
 };
 constexpr int PLAY_GPW_MAX = 64;
-enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4 };
+// game flags: a row queued for the NN, its output ready for the expand, the game's plies done,
+// its row in this cycle's passes, its row held back last cycle (an odd row waits one cycle)
+enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4, PF_EVAL = 8, PF_HELD = 16 };
 constexpr int32_t ERR_SCHED = 16;   // a queue wait timed out (device error word)
 
 struct PlayCtx {
@@ -262,7 +264,24 @@ void k_play(PlayCtx ctx0) {
             if (tid == 0) {   // the queued rows, in game order
                 int n = 0;
                 for (int j = 0; j < ng; ++j)
-                    if (st_f[j] & PF_QUEUED) q_rows[n++] = g0 + j;
+                    if (st_f[j] & PF_QUEUED) ++n;
+                // rows that would leave the last pass partly empty wait one cycle (their games
+                // sit out one search phase: a game's computation is the same whichever cycle
+                // evaluates its row), unless they waited last cycle or there is no full pass
+                int hold = n > NBOARD ? n % NBOARD : 0;
+                for (int j = ng - 1; j >= 0; --j) {
+                    const int fj = st_f[j];
+                    if (!(fj & PF_QUEUED)) continue;
+                    if (hold > 0 && !(fj & PF_HELD)) {
+                        st_f[j] = fj | PF_HELD;
+                        --hold;
+                    } else {
+                        st_f[j] = (fj & ~PF_HELD) | PF_EVAL;
+                    }
+                }
+                n = 0;
+                for (int j = 0; j < ng; ++j)
+                    if (st_f[j] & PF_EVAL) q_rows[n++] = g0 + j;
                 for (int i = n; i < n + 16; ++i) q_rows[i] = -1;
                 s_nq = n;
             }
@@ -295,7 +314,7 @@ void k_play(PlayCtx ctx0) {
                                reinterpret_cast<float*>(smem), vpart, opaque_tid());
             }
             for (int j = tid; j < ng; j += 256)
-                if (st_f[j] & PF_QUEUED) st_f[j] = (st_f[j] & ~PF_QUEUED) | PF_READY;
+                if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
             __syncthreads();
             PT_NOW(t_c4);
             PT_ADD(2, t_c4 - t_c3);
