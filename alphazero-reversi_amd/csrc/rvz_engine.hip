@@ -417,7 +417,8 @@ __device__ __forceinline__ int select_phase(const View& v, int g, int lane, int 
                                              const GameS& root, uint32_t root_meta, int root_n,
                                              uint32_t carry,
                                              XT* __restrict__ leaf_x, int32_t* __restrict__ need,
-                                             unsigned long long& ab) {
+                                             unsigned long long& ab,
+                                             uint64_t* leaf_bits = nullptr) {
     constexpr int NSQ = Geo<BS>::NSQ;
     Node* nodes = v.nodes + (size_t)g * v.M;
     uint32_t* meta = v.meta + (size_t)g * v.M;
@@ -610,7 +611,13 @@ __device__ __forceinline__ int select_phase(const View& v, int g, int lane, int 
                 r = __builtin_amdgcn_readlane(r, 0);
                 if (lane == 0) v.row_of[g] = r;
             }
-            if (lane < NSQ) {
+            if (leaf_bits) {   // k_play: the planes as bitboards (P, O, V) in LDS
+                if (lane == 0) {
+                    leaf_bits[0] = mine(sim);
+                    leaf_bits[1] = theirs(sim);
+                    leaf_bits[2] = V;
+                }
+            } else if (lane < NSQ) {
                 XT* row = leaf_x + (size_t)r * 3 * NSQ;
                 const uint64_t P = mine(sim), O = theirs(sim);
                 row[lane] = (XT)(float)((P >> lane) & 1ull);
@@ -1578,13 +1585,13 @@ static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slo
     dim3 grid;
     if (a.q_next) {     // queue: one persistent workgroup per resident slot, groups of gpw games
         if (a.gpw <= 0) a.gpw = RVZ_PLAY_GROUP;
-        if (a.gpw > PLAY_GPW_MAX) a.gpw = PLAY_GPW_MAX;
+        if (a.gpw > play_gpw_max<F, BS>()) a.gpw = play_gpw_max<F, BS>();
         a.n_groups = (v.G + a.gpw - 1) / a.gpw;
         grid = dim3(a.n_groups < slots ? a.n_groups : slots);
         RVZ_HIP(hipMemsetAsync(a.q_next, 0, sizeof(float) * play_qwords(v.G), e->stream), e);
     } else {            // static: workgroup w owns group w for every ply
         if (a.gpw <= 0) a.gpw = (v.G + slots - 1) / slots;
-        if (a.gpw > PLAY_GPW_MAX) a.gpw = PLAY_GPW_MAX;
+        if (a.gpw > play_gpw_max<F, BS>()) a.gpw = play_gpw_max<F, BS>();
         a.n_groups = (v.G + a.gpw - 1) / a.gpw;
         grid = dim3(a.n_groups);
     }

@@ -420,6 +420,58 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
         out, acc, er, wt, lane, ovf);
 }
 
+// The stem from the leaves' bitboards (the fused self-play kernel: select_phase leaves each
+// queued leaf's (P, O, V) = get_canonical_state()'s three planes, mcts.py:582-594, in LDS): the
+// same A operands stem_h2 builds from the padded float image (0 / 1 in f16, second part 0; the
+// K order of h2_stem_slot), computed from the bits directly.
+template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV>
+__device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
+                                             uint16_t* __restrict__ out, const f16x8 (&w)[CTW][2],
+                                             int wave, int lane, EpiH<CTW, PTW>& er, bool& ovf) {
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
+    typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+    const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
+    const int kg = lane >> 4, ta = 2 * kg, tb = 2 * kg + 1;
+    f16x8 a[PTW][2];
+#pragma unroll
+    for (int u = 0; u < PTW; ++u) {
+        const int px = wt.px[u], b = G::board_of(px), cell = G::cell_of(px);
+        const int r = cell / BS, c = cell % BS;
+        const bool on = px < G::NVALID;
+        uint64_t P = pl[0][0], O = pl[0][1], V = pl[0][2];
+#pragma unroll
+        for (int k = 1; k < NBOARD; ++k)
+            if (b == k) {
+                P = pl[k][0];
+                O = pl[k][1];
+                V = pl[k][2];
+            }
+        auto bit = [&](int t, uint64_t plane) -> uint16_t {
+            const int rr = r + t / 3 - 1, cc = c + t % 3 - 1;
+            const bool in = on && (unsigned)rr < (unsigned)BS && (unsigned)cc < (unsigned)BS;
+            return in && ((plane >> (rr * BS + cc)) & 1ull) ? (uint16_t)0x3C00 : (uint16_t)0;
+        };
+        u16x8 h;
+        h[0] = bit(ta, P);
+        h[1] = bit(ta, O);
+        h[2] = bit(ta, V);
+        h[3] = bit(tb, P);
+        h[4] = bit(tb, O);
+        h[5] = bit(tb, V);
+        h[6] = kg == 0 ? bit(8, P) : (kg == 1 ? bit(8, V) : (uint16_t)0);
+        h[7] = kg == 0 ? bit(8, O) : (uint16_t)0;
+        a[u][0] = __builtin_bit_cast(f16x8, h);
+        a[u][1] = f16x8{};
+    }
+    f32x4 acc[CTW][PTW];
+#pragma unroll
+    for (int c = 0; c < CTW; ++c)
+#pragma unroll
+        for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
+    mma3(acc, a, w);
+    epilogue_h2<F, G::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
+}
+
 template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0,
           bool LASTH = false>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
@@ -585,16 +637,35 @@ struct HeadsGlobalIdx {
     }
 };
 
+// hpv rows straight into the FC heads' LDS input (heads_fc16 with its rows in place): board b
+// is column slot0 + b (< 0 slots: not stored); policy planes at [0, 2 cells), the value plane at
+// PK (the heads' row layout; 8x8: no gaps)
+template <int BS>
+struct HeadsInLds {
+    float* in;
+    int slot0, nslots;
+    __device__ void store(int b, int i, float v) const {
+        constexpr int CELLS = BS * BS, PIN = 2 * CELLS, PK = (PIN + 15) / 16 * 16;
+        constexpr int ROW = heads_in_floats(BS) / 16;
+        const int sl = slot0 + b;
+        if (sl < nslots) in[sl * ROW + (i < PIN ? i : PK + (i - PIN))] = v;
+    }
+};
+
 // One pass of the workgroup (256 threads) over NBOARD boards: board b's leaf planes are row gb[b]
 // of x ([rows][3][BS*BS], gb[b] < 0: no board), its 1x1 head-conv outputs go to row gb[b] of
 // work ([rows][192]: policy planes, then the value plane). smem: CfgH<..>::BYTES of LDS, free on
 // entry and on return. ovf |= an activation overflowed f16 (the caller's sticky word).
-template <int F, int NBOARD, int CTW, int PTW, int BS>
+// Input of a pass: board b's leaf planes are row gb[b] of x (float [rows][3][BS*BS]), or, when
+// bits is set, the bitboards bits[3 * b .. 3 * b + 2] = (P, O, V) (LDS). Output: the 1x1
+// head-conv rows through hout (HeadsGlobalIdx: row gb[b] of work; HeadsInLds: the FC heads' LDS
+// input rows).
+template <int F, int NBOARD, int CTW, int PTW, int BS, class HOut>
 __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
-                                        const int (&gbv)[NBOARD], const float* __restrict__ prm,
-                                        const Layout& L, const uint16_t* __restrict__ blob,
-                                        int n_blocks, float* __restrict__ work, int tid, int lane,
-                                        int wave, bool& ovf) {
+                                        const int (&gbv)[NBOARD], const uint64_t* bits,
+                                        const float* __restrict__ prm, const Layout& L,
+                                        const uint16_t* __restrict__ blob, int n_blocks,
+                                        const HOut& hout, int tid, int lane, int wave, bool& ovf) {
     using WT = WaveTilesH<F, CTW, PTW>;
     constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
@@ -634,18 +705,32 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
                     for (int p = 0; p < 2; ++p) bc[s][c][p] = wr.load(f + (p * C::CT + c) * 64, lane);
             }
         }
-        XinStage<NBOARD, BS, NTHR> st;
-        st.load(x, gb, tid);
         EpiH<CTW, PTW> er;
         f16x8 ws[CTW][2];
-        stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
-        STEM_T(0);
-        st.store(xin, tid);
-        STEM_T(1);
-        __syncthreads();
-        STEM_T(2);
-        stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
-        STEM_T(3);
+        if (bits) {   // leaf bitboards in LDS: no global round trip, no padded image
+            uint64_t pl[NBOARD][3];
+#pragma unroll
+            for (int b = 0; b < NBOARD; ++b)
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    const uint64_t v = bits[3 * b + ch];
+                    pl[b][ch] = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+                }
+            stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+            stem_h2_bits<F, NBOARD, CTW, PTW, BS, ILV>(pl, actA, ws, wave, lane, er, ovf);
+        } else {
+            XinStage<NBOARD, BS, NTHR> st;
+            st.load(x, gb, tid);
+            stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+            STEM_T(0);
+            st.store(xin, tid);
+            STEM_T(1);
+            __syncthreads();
+            STEM_T(2);
+            stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
+            STEM_T(3);
+        }
         __syncthreads();
         PHASE(1);
         const int64_t LW = h2_layer_elems(F);
@@ -685,7 +770,7 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     if (HEPI && n_blocks > 0) {   // the channel-group partials of the last epilogue, + bias, ReLU
         constexpr int CELLS = BS * BS, CG = WT::CG;
         const float* part = reinterpret_cast<const float*>(actA);
-        const HeadsGlobalIdx<NBOARD> hpv{work, gb};
+        const HOut& hpv = hout;
         for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
             const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
             const int b = rem / CELLS, cell = rem % CELLS;
@@ -698,8 +783,8 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
         }
     } else {
         head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA},
-                                                  reinterpret_cast<float*>(actB), prm, L,
-                                                  HeadsGlobalIdx<NBOARD>{work, gb}, tid);
+                                                  reinterpret_cast<float*>(actB), prm, L, hout,
+                                                  tid);
     }
 }
 

@@ -47,6 +47,14 @@ struct PlayArgs {
     int n_groups;
 };
 constexpr int PLAY_GPW_MAX = 64;
+// the 8x8 / 64-filter (C2) geometry keeps its head-conv rows in LDS for the FC heads (no
+// workspace round trip): at most 8 games per workgroup, so that 8 rows of LDS hold a cycle's rows
+template <int F, int BS>
+__host__ __device__ constexpr bool play_heads_lds() { return F == 64 && BS == 8; }
+template <int F, int BS>
+__host__ __device__ constexpr int play_gpw_max() {
+    return play_heads_lds<F, BS>() ? 8 : PLAY_GPW_MAX;
+}
 // game flags: a row queued for the NN, its output ready for the expand, the game's plies done,
 // its row in this cycle's passes, its row held back last cycle (an odd row waits one cycle)
 enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4, PF_EVAL = 8, PF_HELD = 16 };
@@ -97,16 +105,22 @@ void k_play(PlayCtx ctx0) {
     using GH = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     using C = CfgH<F, GH::NPIX>;
     constexpr int NPOL = Geo<BS>::NPOL;
+    constexpr bool HLDS = play_heads_lds<F, BS>();
+    constexpr int GMAX = play_gpw_max<F, BS>();
+    constexpr int HROW = heads_in_floats(BS) / 16;
     // LDS: the trunk's activation image; between passes its head holds the search phase's act /
-    // reset scratch (per wave) or the FC heads' input rows
+    // reset scratch (per wave) or (not HLDS) the FC heads' input rows
     constexpr int SP_BYTES = WPB * (NPOL + 7) * 8;
     static_assert(heads_in_floats(BS) * 4 <= C::BYTES, "heads rows fit");
     static_assert(SP_BYTES + WPB * 624 * 4 <= C::BYTES, "act / reset scratch fits");
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
-    __shared__ int st_k[PLAY_GPW_MAX];   // next batch of the game's search (E: act next)
-    __shared__ int st_f[PLAY_GPW_MAX];   // PF_* flags
-    __shared__ int st_p[PLAY_GPW_MAX];   // plies committed in this launch
-    __shared__ int q_rows[PLAY_GPW_MAX + 16];
+    __shared__ int st_k[GMAX];   // next batch of the game's search (E: act next)
+    __shared__ int st_f[GMAX];   // PF_* flags
+    __shared__ int st_p[GMAX];   // plies committed in this launch
+    __shared__ uint64_t st_bits[GMAX * 3];              // the queued leaf's (P, O, V) per game
+    __shared__ uint64_t q_bits[(GMAX + NBOARD) * 3];    // the same, in this cycle's row order
+    __shared__ __attribute__((aligned(16))) float hin[HLDS ? GMAX * HROW : 4];   // heads rows
+    __shared__ int q_rows[GMAX + 16];
     __shared__ int s_nq;
     __shared__ float vpart[4][16];
     __shared__ int s_task[2];
@@ -213,7 +227,7 @@ void k_play(PlayCtx ctx0) {
                         const int bsz = min(a.B, a.S - k * a.B);
                         const int copies = select_phase<BS, float>(v, g, lane, first, bsz, k, root,
                                                                    root_meta, root_n, carry, a.x,
-                                                                   a.need, ab);
+                                                                   a.need, ab, st_bits + 3 * j);
                         ++k;
                         // the last batch's row with skip_last: left unevaluated (rvz_search_skip)
                         if (copies > 0 && !(k == E && a.skip_last)) {
@@ -281,8 +295,12 @@ void k_play(PlayCtx ctx0) {
                 }
                 n = 0;
                 for (int j = 0; j < ng; ++j)
-                    if (st_f[j] & PF_EVAL) q_rows[n++] = g0 + j;
+                    if (st_f[j] & PF_EVAL) {
+                        for (int ch = 0; ch < 3; ++ch) q_bits[3 * n + ch] = st_bits[3 * j + ch];
+                        q_rows[n++] = g0 + j;
+                    }
                 for (int i = n; i < n + 16; ++i) q_rows[i] = -1;
+                for (int i = 3 * n; i < 3 * (n + NBOARD); ++i) q_bits[i] = 0;
                 s_nq = n;
             }
             __syncthreads();
@@ -298,9 +316,16 @@ void k_play(PlayCtx ctx0) {
 #pragma unroll
                 for (int k = 0; k < NBOARD; ++k) gb[k] = q_rows[p0 + k];
                 const int t = opaque_tid();
-                h2_pass<F, NBOARD, CTW, PTW, BS>(smem, a.x, gb, a.prm, a.L, a.blob, a.n_blocks,
-                                                 a.work, t, t & 63,
-                                                 __builtin_amdgcn_readfirstlane(t >> 6), ovf);
+                if constexpr (HLDS)
+                    h2_pass<F, NBOARD, CTW, PTW, BS>(
+                        smem, a.x, gb, q_bits + 3 * p0, a.prm, a.L, a.blob, a.n_blocks,
+                        HeadsInLds<BS>{hin, p0, nq}, t, t & 63,
+                        __builtin_amdgcn_readfirstlane(t >> 6), ovf);
+                else
+                    h2_pass<F, NBOARD, CTW, PTW, BS>(
+                        smem, a.x, gb, q_bits + 3 * p0, a.prm, a.L, a.blob, a.n_blocks,
+                        HeadsGlobalIdx<NBOARD>(a.work, gb), t, t & 63,
+                        __builtin_amdgcn_readfirstlane(t >> 6), ovf);
                 __syncthreads();
             }
             PT_NOW(t_c3);
@@ -309,9 +334,14 @@ void k_play(PlayCtx ctx0) {
             PT_ADD(6, nq);
             for (int h0 = 0; h0 < nq; h0 += 16) {
                 const PlayArgs& a = play_ctx().a;
-                heads_fc16<BS, HeadRowsList, false>(a.work, HeadRowsList{q_rows + h0}, a.prm, a.L,
-                                                a.logits, a.value,
-                               reinterpret_cast<float*>(smem), vpart, opaque_tid());
+                if constexpr (HLDS)   // the rows are in hin already (HeadsInLds); columns >= 8 mirror 0-7
+                    heads_fc16<BS, HeadRowsList, false, false, GMAX>(
+                        a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value, hin,
+                        vpart, opaque_tid());
+                else
+                    heads_fc16<BS, HeadRowsList, false, true>(
+                        a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
+                        reinterpret_cast<float*>(smem), vpart, opaque_tid());
             }
             for (int j = tid; j < ng; j += 256)
                 if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;

@@ -76,8 +76,8 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     int gb[NBOARD];
 #pragma unroll
     for (int k = 0; k < NBOARD; ++k) gb[k] = g0 + k < n_boards ? g0 + k : -1;
-    h2_pass<F, NBOARD, CTW, PTW, BS>(smem, x, gb, prm, L, blob, n_blocks, work, tid, lane, wave,
-                                     ovf);
+    h2_pass<F, NBOARD, CTW, PTW, BS>(smem, x, gb, nullptr, prm, L, blob, n_blocks,
+                                     HeadsGlobalIdx<NBOARD>(work, gb), tid, lane, wave, ovf);
     PHASE(3);
     RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1

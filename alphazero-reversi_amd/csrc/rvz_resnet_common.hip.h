@@ -165,7 +165,12 @@ __host__ __device__ constexpr int heads_in_floats(int BS) {
 // STREAM: the weight fragments streamed RVZ_HEADS_PD steps ahead (76 VGPRs: k_heads_mfma's
 // waves fit beside two trunk waves), or all issued up front (one L2 round trip; ~148 VGPRs: the
 // fused k_play, whose register budget is the trunk's)
-template <int BS, class Rows, bool STREAM = RVZ_HEADS_STREAM != 0>
+// COPY: the 16 rows are copied from the workspace into `in`; false: they are there already
+// (the fused kernel's head convs wrote them, HeadsInLds)
+// INROWS < 16: `in` holds INROWS rows and column c reads row c % INROWS (columns past the
+// rows are not stored: their outputs are discarded)
+template <int BS, class Rows, bool STREAM = RVZ_HEADS_STREAM != 0, bool COPY = true,
+          int INROWS = 16>
 __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const Rows& rmap,
                                            const float* __restrict__ prm, const Layout& L,
                                            float* __restrict__ logits, float* __restrict__ value,
@@ -235,7 +240,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
     }
     }
 
-    {   // the 16 workspace rows into LDS, 16 B per load, all loads in flight before the stores
+    if constexpr (COPY) {   // the 16 workspace rows into LDS, 16 B per load, all in flight
         // (policy planes at k < PIN, the value plane at PK.., zeros between)
         constexpr int RQ = (PK + VK) / 4, NQ = 16 * RQ / 256;
         static_assert(16 * RQ % 256 == 0 && PK % 4 == 0 && ROW % 4 == 0, "whole float4 rounds");
@@ -256,7 +261,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
         }
     }
     __syncthreads();
-    const float* inb = in + col * ROW + 4 * grp;
+    const float* inb = in + (col % INROWS) * ROW + 4 * grp;
     float vp = 0.0f;
     if constexpr (STREAM) {
     f32x4 acc = {};
