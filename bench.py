@@ -101,9 +101,10 @@ def parse(argv=None):
     ap.add_argument("--lanes", type=int, default=None,
                     help="independent game lanes per GPU, one stream each "
                          "(rvz.LaneRunner); the games are the same as with one lane")
-    ap.add_argument("--plies-per-graph", type=int, default=1,
+    ap.add_argument("--plies-per-graph", type=int, default=0,
                     help="plies captured into each lane's HIP graph (one replay plays them all; "
-                         "--steps must be a multiple)")
+                         "--steps must be a multiple; 0: --fused one launch for all --steps, "
+                         "else 1)")
     ap.add_argument("--fused", action="store_true",
                     help="one rvz_play launch per ply: each workgroup plays its own games (search "
                          "+ h2 evaluator + act + autoreset in one persistent kernel)")
@@ -522,7 +523,8 @@ def selfplay(args, device, rank, world, full=True):
     # kernel's duration over every lane-0 launch of the timed region
     graph_events = []
     cap_kw = {"free_run": not args.joined_lanes} if args.lanes > 1 else {}
-    ppg = 1 if args.no_graph else args.plies_per_graph
+    ppg = args.plies_per_graph or (args.steps if args.fused else 1)
+    ppg = 1 if args.no_graph else ppg
     if args.steps % ppg:
         raise SystemExit(f"--steps {args.steps} is not a multiple of --plies-per-graph {ppg}")
     cap_kw["plies"] = ppg
@@ -652,7 +654,8 @@ def selfplay(args, device, rank, world, full=True):
            # host time to enqueue the timed plies (graph replays): below ms_per_step, the device
            # never waits for the host
            "host_enqueue_ms_per_step": round((t_enq[-1] - t0) / max(1, args.steps) * 1e3, 3),
-           "plies_per_graph": ppg}
+           "plies_per_graph": ppg,
+           "play_group": args.play_group if args.fused else None}
     if full:
         kernels = {}
         for k in ("step", "act"):
@@ -891,7 +894,7 @@ def main():
                        "nn": f"{args.blocks}x{args.filters}",
                        "nn_kernel": ("k_play (h2_pass + heads_fc16 inside the fused self-play "
                                      "launch)" if args.fused else "rvz_resnet_fwd_h2"),
-                       "fused": args.fused, "plies_per_graph": args.plies_per_graph,
+                       "fused": args.fused, "plies_per_graph": r["plies_per_graph"],
                        "graph": not args.no_graph, "lanes": args.lanes,
                        "lane_graphs": ("joined" if args.joined_lanes else "free")
                        if args.lanes > 1 else None,
