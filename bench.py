@@ -46,13 +46,17 @@ PRESETS = {   # BASELINE.json configs
     # lanes: independent game lanes per GPU (same games; measured best per config)
     # c1: the reference's own plumbing case (one game, 100 sims, the ModelConfig default 5x128
     # net; config.py:14-15) on one GPU, with the CPU port on the same single game beside it
-    "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1),
-    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2),
-    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1),
+    "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1, fused=False),
+    # fused: the fused self-play launch (k_play) measures faster at C2 (r03o: +4-5% over 2
+    # lanes); at C3 (one 27k-row trunk launch per batch, no ramp/tail to remove) and C5 (86 KB of
+    # LDS: one workgroup per CU, nothing covers the search phases) the launches are faster
+    "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2, fused=True,
+               play_group=-6),
+    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, fused=False),
     # per GPU, x8; a step = one self-play + training iteration (main_c4)
     "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, steps=1,
-               warmup=0),
-    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2),
+               warmup=0, fused=False),
+    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2, fused=False),
 }
 # measured beside the headline in the default N = 1 line (the largest single-GPU config and the
 # 6x6 variant); each is a full workload of its preset over the same --steps
@@ -105,10 +109,13 @@ def parse(argv=None):
                     help="plies captured into each lane's HIP graph (one replay plays them all; "
                          "--steps must be a multiple; 0: --fused one launch for all --steps, "
                          "else 1)")
-    ap.add_argument("--fused", action="store_true",
-                    help="one rvz_play launch per ply: each workgroup plays its own games (search "
-                         "+ h2 evaluator + act + autoreset in one persistent kernel)")
-    ap.add_argument("--play-group", type=int, default=0,
+    ap.add_argument("--fused", dest="fused", action="store_true", default=None,
+                    help="the fused self-play launch (rvz_play): each workgroup plays its own "
+                         "games, search + h2 evaluator + act + autoreset in one persistent kernel "
+                         "(the preset decides by default: C2 fused, C1/C3/C4/C5 not)")
+    ap.add_argument("--no-fused", dest="fused", action="store_false",
+                    help="the pull-style per-batch launches (k_step / trunk / heads per lane)")
+    ap.add_argument("--play-group", type=int, default=None,
                     help="--fused: rvz_play games_per_workgroup (> 0 static ownership; <= 0 the "
                          "task queue with groups of -N games, 0 the default)")
     ap.add_argument("--joined-lanes", action="store_true",
@@ -156,8 +163,8 @@ def set_evals(args, mode):
 
 
 def apply_preset(args, name):
-    for k, v in dict(dict(steps=60, warmup=3), **PRESETS[name]).items():
-        if getattr(args, k) is None:
+    for k, v in dict(dict(steps=60, warmup=3, play_group=0), **PRESETS[name]).items():
+        if getattr(args, k, None) is None:
             setattr(args, k, v)
 
 
@@ -628,7 +635,8 @@ def selfplay(args, device, rank, world, full=True):
     ach = fpr * rows_tr / (t_tr * 1e-3) / 1e12
     ach_u = upr * rows_tr / (t_tr * 1e-3) / 1e12
     region = fpr * rows / (t1 - t0) / 1e12      # every lane's evaluated rows / timed wall time
-    traffic, traffic_src = (stored_traffic(args, "nn_trunk") if full else (None, None))
+    traffic, traffic_src = (stored_traffic(args, "play" if args.fused else "nn_trunk")
+                            if full else (None, None))
     roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma",
             "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4),
@@ -693,7 +701,7 @@ def selfplay(args, device, rank, world, full=True):
 def sub_config(base, name, device, rank, world):
     """A preset measured beside the headline: the same harness, its own net and engines."""
     a = copy.copy(base)
-    for k in ("games", "sims", "blocks", "filters", "board", "lanes"):
+    for k in ("games", "sims", "blocks", "filters", "board", "lanes", "fused", "play_group"):
         setattr(a, k, None)
     a.config = name
     a.stamps_dump = None

@@ -3,7 +3,7 @@
 set -u
 OUT=${OUT:-gpurun_out}; TAG=${TAG:-r01}
 mkdir -p "$OUT"; export TMPDIR=/tmp
-ARGS="--steps 4 --warmup 1 --no-cpu-baseline --instrument-plies 1 --no-evals-ab --sub-configs none ${BENCH_ARGS:-}"
+ARGS="--no-cpu-baseline --instrument-plies 1 --no-evals-ab --sub-configs none ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run \
     -- python bench.py $ARGS > "$OUT/pmc_fetch_$TAG.json" 2> "$OUT/pmc_fetch_$TAG.err"
 rc=$?; echo "fetch_rc=$rc"; [ $rc -ne 0 ] && exit $rc

@@ -16,7 +16,10 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"step": "k_step<", "act": "k_act<", "expand_backup": "k_expand_backup<",
+# play: the fused self-play launch; its mean is over the last LAST_PLAY dispatches (bench.py's
+# --steps-ply launches: the warm-up replays and the timed one; the first eager ply is shorter)
+LAST_PLAY = 3
+KERNELS = {"play": "k_play<", "step": "k_step<", "act": "k_act<", "expand_backup": "k_expand_backup<",
            "reset": "k_reset<", "nn_trunk": ("k_resnet_h2<", "k_resnet_split<"), "nn_heads": "k_heads_fc(",
            "nn_conv3x3": "igemm_fwd_gtcx35_nhwc_fp32_bx0_ex1_bt128x64x16"}
 
@@ -24,13 +27,14 @@ KERNELS = {"step": "k_step<", "act": "k_act<", "expand_backup": "k_expand_backup
 def load(run_dir, counter):
     files = glob.glob(os.path.join(run_dir, "**", "*counter_collection.csv"), recursive=True)
     per = defaultdict(list)
-    for f in files:
-        for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") != counter:
-                continue
-            for key, pat in KERNELS.items():
-                if any(p in r["Kernel_Name"] for p in ((pat,) if isinstance(pat, str) else pat)):
-                    per[key].append(float(r["Counter_Value"]))
+    rows = [r for f in files for r in csv.DictReader(open(f))]
+    rows.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))   # dispatch order
+    for r in rows:
+        if r.get("Counter_Name") != counter:
+            continue
+        for key, pat in KERNELS.items():
+            if any(p in r["Kernel_Name"] for p in ((pat,) if isinstance(pat, str) else pat)):
+                per[key].append(float(r["Counter_Value"]))
     return per
 
 
@@ -42,8 +46,11 @@ def main():
     for key in KERNELS:
         if not fetch.get(key) or not write.get(key):
             continue
-        f = sum(fetch[key]) / len(fetch[key])
-        w = sum(write[key]) / len(write[key])
+        fk, wk = fetch[key], write[key]
+        if key == "play":
+            fk, wk = fk[-LAST_PLAY:], wk[-LAST_PLAY:]
+        f = sum(fk) / len(fk)
+        w = sum(wk) / len(wk)
         res[key] = {"dispatches": len(fetch[key]), "FETCH_SIZE_KB": round(f, 2),
                     "WRITE_SIZE_KB": round(w, 2),
                     "raw_bytes_per_launch": round((f + w) * 1024),
