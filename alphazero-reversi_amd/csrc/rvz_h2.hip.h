@@ -652,6 +652,18 @@ struct HeadsInLds {
     }
 };
 
+// RVZ_PLAY_TIMING (tools/exp_play_phases.py): shader clocks of a pass's parts per workgroup,
+// [0] zero rows + stem (to its barrier), [1] [0] + the residual tower, [2] 1x1 head convs,
+// [3] passes
+#ifdef RVZ_PLAY_TIMING
+__device__ unsigned long long g_pass_t[16384][4];
+#define PASS_NOW(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
+#define PASS_ADD(i, v) if (threadIdx.x == 0 && blockIdx.x < 16384) g_pass_t[blockIdx.x][i] += (v)
+#else
+#define PASS_NOW(t)
+#define PASS_ADD(i, v)
+#endif
+
 // One pass of the workgroup (256 threads) over NBOARD boards: board b's leaf planes are row gb[b]
 // of x ([rows][3][BS*BS], gb[b] < 0: no board), its 1x1 head-conv outputs go to row gb[b] of
 // work ([rows][192]: policy planes, then the value plane). smem: CfgH<..>::BYTES of LDS, free on
@@ -678,6 +690,7 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
 #pragma unroll
     for (int k = 0; k < NBOARD; ++k) gb[k] = __builtin_amdgcn_readfirstlane(gbv[k]);
 
+    PASS_NOW(tp0);
     // zero rows of both buffers, both parts, every k-step plane (4 * KS planes of KSP)
     for (int i = tid; i < 4 * C::KS * 8 * H2_K; i += NTHR) {
         const int plane = i / (8 * H2_K), k = i % (8 * H2_K);
@@ -733,6 +746,10 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
         }
         __syncthreads();
         PHASE(1);
+        {
+            PASS_NOW(tp1);
+            PASS_ADD(0, tp1 - tp0);
+        }
         const int64_t LW = h2_layer_elems(F);
         const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
         for (int blk = 0; blk < n_blocks - (HEPI ? 1 : 0); ++blk) {
@@ -766,6 +783,8 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     else
         trunk(std::integral_constant<int, 0>{});
     PHASE(2);
+    PASS_NOW(tp2);
+    PASS_ADD(1, tp2 - tp0);   // stem + tower
     // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
     if (HEPI && n_blocks > 0) {   // the channel-group partials of the last epilogue, + bias, ReLU
         constexpr int CELLS = BS * BS, CG = WT::CG;
@@ -786,6 +805,13 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
                                                   reinterpret_cast<float*>(actB), prm, L, hout,
                                                   tid);
     }
+#ifdef RVZ_PLAY_TIMING
+    {
+        PASS_NOW(tp3);
+        PASS_ADD(2, tp3 - tp2);
+        PASS_ADD(3, 1);
+    }
+#endif
 }
 
 // RVZ_H2_MAXV (experiments): cap the trunk's VGPRs so that a k_step wave (80) fits on a SIMD

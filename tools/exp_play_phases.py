@@ -25,11 +25,12 @@ net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
 eng = rvz.Engine(G, S, 64, memo=True)
 run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=42,
                          skip_last_eval=True, fused=True)
+run.play_group = int(os.environ.get("GROUP", -6))
 run.start()
 lib = rvz.load()
 lib.rvz_play_timing_read.argtypes = [C.c_void_p, C.c_int]
 n_wg = 16384
-buf = np.zeros((n_wg, 8), dtype=np.uint64)
+buf = np.zeros((n_wg, 12), dtype=np.uint64)   # [n][8] phases, then [n][4] pass parts
 for _ in range(WARM):
     run.ply()
 torch.cuda.synchronize()
@@ -38,13 +39,17 @@ t0 = torch.cuda.Event(enable_timing=True)
 t1 = torch.cuda.Event(enable_timing=True)
 t0.record()
 eng.play(run.evaluator, PLIES, 1.0, run.seeds, run.seed_stride, run._plies, run._done,
-         reset=True, skip_last_eval=True)
+         reset=True, skip_last_eval=True, games_per_workgroup=run.play_group)
 t1.record()
 torch.cuda.synchronize()
 ms = t0.elapsed_time(t1)
 lib.rvz_play_timing_read(buf.ctypes.data, n_wg)
+flat = buf.reshape(-1)
+pt = flat[n_wg * 8:n_wg * 12].reshape(n_wg, 4).astype(np.float64)
+buf = flat[:n_wg * 8].reshape(n_wg, 8)
 used = buf[:, 3] > 0
 b = buf[used].astype(np.float64)
+pt = pt[used]
 tot = b[:, 3]
 out = {"workgroups": int(used.sum()), "launch_ms": round(ms, 3), "plies": PLIES,
        "clock_GHz_est": round(float(np.median(tot)) / (ms * 1e6), 3),
@@ -57,6 +62,9 @@ out = {"workgroups": int(used.sum()), "launch_ms": round(ms, 3), "plies": PLIES,
        "trunk_kcycles_per_pass": round(float(b[:, 1].sum() / b[:, 5].sum()) / 1e3, 2),
        "search_kcycles_per_cycle": round(float(b[:, 0].sum() / b[:, 4].sum()) / 1e3, 2),
        "heads_kcycles_per_cycle": round(float(b[:, 2].sum() / b[:, 4].sum()) / 1e3, 2),
+       "pass_stem_kcycles": round(float(pt[:, 0].sum() / pt[:, 3].sum()) / 1e3, 2),
+       "pass_tower_kcycles": round(float((pt[:, 1] - pt[:, 0]).sum() / pt[:, 3].sum()) / 1e3, 2),
+       "pass_headconv_kcycles": round(float(pt[:, 2].sum() / pt[:, 3].sum()) / 1e3, 2),
        "wg_total_kcycles_min_med_max": [round(float(x) / 1e3, 1)
                                         for x in (tot.min(), np.median(tot), tot.max())]}
 print(json.dumps(out))
