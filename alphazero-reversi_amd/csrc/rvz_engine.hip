@@ -1604,15 +1604,16 @@ static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slo
 }  // extern "C++"
 
 #ifdef RVZ_PLAY_TIMING
-// tools/exp_play_phases.py: host copy of g_play_t (n workgroups x 8), then zeroed
+// tools/exp_play_phases.py: host copy of g_play_t (n workgroups x 12) and g_pass_t (n x 6), then
+// zeroed
 int rvz_play_timing_read(uint64_t* host, int n) {
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_play_t), (size_t)n * 8 * 8) != hipSuccess)
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_play_t), (size_t)n * 12 * 8) != hipSuccess)
         return RVZ_EHIP;
-    if (hipMemcpyFromSymbol(host + (size_t)n * 8, HIP_SYMBOL(g_pass_t), (size_t)n * 4 * 8) !=
+    if (hipMemcpyFromSymbol(host + (size_t)n * 12, HIP_SYMBOL(g_pass_t), (size_t)n * 6 * 8) !=
         hipSuccess)
         return RVZ_EHIP;
-    std::vector<unsigned long long> z((size_t)16384 * 8, 0ull);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pass_t), z.data(), (size_t)16384 * 4 * 8) != hipSuccess)
+    std::vector<unsigned long long> z((size_t)16384 * 12, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pass_t), z.data(), (size_t)16384 * 6 * 8) != hipSuccess)
         return RVZ_EHIP;
     return hipMemcpyToSymbol(HIP_SYMBOL(g_play_t), z.data(), z.size() * 8) == hipSuccess
                ? RVZ_OK : RVZ_EHIP;

@@ -334,11 +334,13 @@ __device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
 // the three partial products, consecutive MFMAs on different accumulators
 // (U0 = 1: pixel tile 0 skipped, its tap is off the boards for the whole tile)
 // (issue order measured neutral: pixel- or channel-major within a k-step, 0.1% either way)
-template <int CTW, int PTW, int U0 = 0>
+// (NT = 2: the activations' second part is zero — the bitboard stem's 0 / 1 inputs — so its
+// product w0 x1 would add exact zeros to accumulators that are never -0: left out)
+template <int CTW, int PTW, int U0 = 0, int NT = 3>
 __device__ __forceinline__ void mma3(f32x4 (&acc)[CTW][PTW], const f16x8 (&a)[PTW][2],
                                      const f16x8 (&w)[CTW][2]) {
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
@@ -468,7 +470,7 @@ __device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
     for (int c = 0; c < CTW; ++c)
 #pragma unroll
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
-    mma3(acc, a, w);
+    mma3<CTW, PTW, 0, 2>(acc, a, w);
     epilogue_h2<F, G::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
 }
 
@@ -651,18 +653,6 @@ struct HeadsInLds {
         if (sl < nslots) in[sl * ROW + (i < PIN ? i : PK + (i - PIN))] = v;
     }
 };
-
-// RVZ_PLAY_TIMING (tools/exp_play_phases.py): shader clocks of a pass's parts per workgroup,
-// [0] zero rows + stem (to its barrier), [1] [0] + the residual tower, [2] 1x1 head convs,
-// [3] passes
-#ifdef RVZ_PLAY_TIMING
-__device__ unsigned long long g_pass_t[16384][4];
-#define PASS_NOW(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
-#define PASS_ADD(i, v) if (threadIdx.x == 0 && blockIdx.x < 16384) g_pass_t[blockIdx.x][i] += (v)
-#else
-#define PASS_NOW(t)
-#define PASS_ADD(i, v)
-#endif
 
 // One pass of the workgroup (256 threads) over NBOARD boards: board b's leaf planes are row gb[b]
 // of x ([rows][3][BS*BS], gb[b] < 0: no board), its 1x1 head-conv outputs go to row gb[b] of

@@ -86,9 +86,10 @@ __device__ __forceinline__ const PlayCtx& play_ctx() {
 // RVZ_PLAY_TIMING (tools/exp_play_phases.py, instrumented builds only): per workgroup, shader
 // clocks (s_memtime) spent in [0] the search phase (to its barrier), [1] the trunk passes,
 // [2] the FC heads, [3] the whole launch; [4] cycles of the loop, [5] trunk passes, [6] rows,
-// [7] the workgroup's XCC / CU (HW_ID)
+// [7] the workgroup's XCC / CU (HW_ID); [8] cycles waiting for a task's previous ply (queue),
+// [9] tasks, [10] the launch clock at the workgroup's end (s_memrealtime, 100 MHz)
 #ifdef RVZ_PLAY_TIMING
-__device__ unsigned long long g_play_t[16384][8];
+__device__ unsigned long long g_play_t[16384][12];
 #define PT_NOW(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
 #define PT_ADD(i, v) if (tid == 0 && blockIdx.x < 16384) g_play_t[blockIdx.x][i] += (v)
 #else
@@ -149,6 +150,7 @@ void k_play(PlayCtx ctx0) {
             gi = blockIdx.x;
             ply0 = 0;
         } else {
+            PT_NOW(t_q0);
             if (tid == 0) {
                 const PlayArgs& a = play_ctx().a;
                 const unsigned t = __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
@@ -180,6 +182,9 @@ void k_play(PlayCtx ctx0) {
             gi = __builtin_amdgcn_readfirstlane(s_task[0]);
             ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
             if (gi < 0) break;
+            PT_NOW(t_q1);
+            PT_ADD(8, t_q1 - t_q0);
+            PT_ADD(9, 1);
         }
         const int g0 = gi * gpw;
         const int ng = min(gpw, G - g0);
@@ -364,6 +369,8 @@ void k_play(PlayCtx ctx0) {
     {
         PT_NOW(t_end);
         PT_ADD(3, t_end - t_start);
+        if (tid == 0 && blockIdx.x < 16384)
+            g_play_t[blockIdx.x][10] = __builtin_amdgcn_s_memrealtime();
         if (tid == 0 && blockIdx.x < 16384)
             g_play_t[blockIdx.x][7] =
                 ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |

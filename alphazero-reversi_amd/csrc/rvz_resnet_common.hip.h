@@ -116,6 +116,18 @@ struct HeadsGlobal {     // hpv rows in the global workspace of rvz_resnet_fwd_s
     }
 };
 
+// RVZ_PLAY_TIMING (tools/exp_play_phases.py): shader clocks of a fused trunk pass's parts per
+// workgroup, [0] zero rows + stem (to its barrier), [1] [0] + the residual tower, [2] 1x1 head
+// convs, [3] passes; of the FC heads (held weights), [4] to the weights' arrival, [5] the rest
+#ifdef RVZ_PLAY_TIMING
+__device__ unsigned long long g_pass_t[16384][6];
+#define PASS_NOW(t) const unsigned long long t = __builtin_amdgcn_s_memtime()
+#define PASS_ADD(i, v) if (threadIdx.x == 0 && blockIdx.x < 16384) g_pass_t[blockIdx.x][i] += (v)
+#else
+#define PASS_NOW(t)
+#define PASS_ADD(i, v)
+#endif
+
 // a compacted leaf batch (include/rvz.h RVZ_LIVE_STRIPE): is the row past its stripe's live count?
 __device__ __forceinline__ bool row_dead(const int32_t* __restrict__ n_live, int row) {
     return n_live && row % RVZ_LIVE_STRIPE >= n_live[row / RVZ_LIVE_STRIPE * RVZ_LIVE_PITCH];
@@ -185,6 +197,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
     const int lane = tid & 63, wave = tid >> 6;
     const int col = lane & 15, grp = lane >> 4;
     const int grow = rmap.row(col);                  // this lane's board column: its row
+    PASS_NOW(th0);
 
     // the wave's weight steps in order: value fc1 tiles wave + 4m (VJ steps each), then policy
     // tiles wave + 4m (PJ steps each); step s = one f32x4 of the A row (unit 16 t + col,
@@ -261,6 +274,11 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
         }
     }
     __syncthreads();
+#ifdef RVZ_PLAY_TIMING
+    if constexpr (!STREAM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    PASS_NOW(th1);
+    if constexpr (!STREAM) PASS_ADD(4, th1 - th0);
     const float* inb = in + (col % INROWS) * ROW + 4 * grp;
     float vp = 0.0f;
     if constexpr (STREAM) {
@@ -361,6 +379,8 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
                               prm[L.vfc2_b]);
     }
     __syncthreads();
+    PASS_NOW(th2);
+    if constexpr (!STREAM) PASS_ADD(5, th2 - th1);
 }
 
 template <int BS>

@@ -30,7 +30,7 @@ run.start()
 lib = rvz.load()
 lib.rvz_play_timing_read.argtypes = [C.c_void_p, C.c_int]
 n_wg = 16384
-buf = np.zeros((n_wg, 12), dtype=np.uint64)   # [n][8] phases, then [n][4] pass parts
+buf = np.zeros((n_wg, 18), dtype=np.uint64)   # [n][12] phases, then [n][6] pass / heads parts
 for _ in range(WARM):
     run.ply()
 torch.cuda.synchronize()
@@ -45,10 +45,11 @@ torch.cuda.synchronize()
 ms = t0.elapsed_time(t1)
 lib.rvz_play_timing_read(buf.ctypes.data, n_wg)
 flat = buf.reshape(-1)
-pt = flat[n_wg * 8:n_wg * 12].reshape(n_wg, 4).astype(np.float64)
-buf = flat[:n_wg * 8].reshape(n_wg, 8)
+pt = flat[n_wg * 12:n_wg * 18].reshape(n_wg, 6).astype(np.float64)
+buf = flat[:n_wg * 12].reshape(n_wg, 12)
 used = buf[:, 3] > 0
 b = buf[used].astype(np.float64)
+end_us = (b[:, 10] - b[:, 10].max()) / 100.0   # s_memrealtime ticks (100 MHz) before the last end
 pt = pt[used]
 tot = b[:, 3]
 out = {"workgroups": int(used.sum()), "launch_ms": round(ms, 3), "plies": PLIES,
@@ -65,6 +66,12 @@ out = {"workgroups": int(used.sum()), "launch_ms": round(ms, 3), "plies": PLIES,
        "pass_stem_kcycles": round(float(pt[:, 0].sum() / pt[:, 3].sum()) / 1e3, 2),
        "pass_tower_kcycles": round(float((pt[:, 1] - pt[:, 0]).sum() / pt[:, 3].sum()) / 1e3, 2),
        "pass_headconv_kcycles": round(float(pt[:, 2].sum() / pt[:, 3].sum()) / 1e3, 2),
+       "heads_weights_wait_kcycles_per_cycle": round(float(pt[:, 4].sum() / b[:, 4].sum()) / 1e3, 2),
+       "heads_compute_kcycles_per_cycle": round(float(pt[:, 5].sum() / b[:, 4].sum()) / 1e3, 2),
+       "queue_wait_frac": round(float((b[:, 8] / tot).mean()), 4),
+       "tasks_per_wg_min_med_max": [int(b[:, 9].min()), int(np.median(b[:, 9])), int(b[:, 9].max())],
+       "wg_end_us_before_last_median_max": [round(float(-np.median(end_us)), 1),
+                                             round(float(-end_us.min()), 1)],
        "wg_total_kcycles_min_med_max": [round(float(x) / 1e3, 1)
                                         for x in (tot.min(), np.median(tot), tot.max())]}
 print(json.dumps(out))
