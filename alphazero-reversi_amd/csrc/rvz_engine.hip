@@ -139,7 +139,16 @@ __device__ unsigned long long g_wtime[WALK_STATS_MAX][5];
 #define WT_NOW(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define WT_ADD(i, t0) \
     if (lane == 0 && g < WALK_STATS_MAX) g_wtime[g][i] += __builtin_amdgcn_s_memtime() - (t0)
+// the fused kernel's game steps (k_play, tools/exp_play_walks.py): [0] expand, [1] act +
+// autoreset, [2] the whole step (a game's turn in one search phase), [3] steps
+__device__ unsigned long long g_ftime[WALK_STATS_MAX][4];
+#define FT_ADD(i, t0) \
+    if (lane == 0 && g < WALK_STATS_MAX) g_ftime[g][i] += __builtin_amdgcn_s_memtime() - (t0)
+#define FT_CNT() \
+    if (lane == 0 && g < WALK_STATS_MAX) g_ftime[g][3] += 1
 #else
+#define FT_ADD(i, t0)
+#define FT_CNT()
 #define WALK_STAT(i, k)
 #define WT_NOW(t)
 #define WT_ADD(i, t0)
@@ -1527,6 +1536,26 @@ int rvz_walk_times(int32_t n_games, int64_t* out11) {
     std::vector<unsigned long long> z((size_t)WALK_STATS_MAX * 5, 0ull);
     return hipMemcpyToSymbol(HIP_SYMBOL(g_wtime), z.data(), z.size() * 8) == hipSuccess
                ? RVZ_OK : RVZ_EHIP;
+}
+#endif
+
+#ifdef RVZ_WALK_STATS
+// tools/exp_play_walks.py: host uint64 [n][9] = g_wtime's 5 columns, then g_ftime's 4; zeroes both
+int rvz_play_walk_read(int32_t n_games, uint64_t* out) {
+    const int n = n_games < WALK_STATS_MAX ? n_games : WALK_STATS_MAX;
+    std::vector<unsigned long long> a((size_t)n * 5), b((size_t)n * 4);
+    if (hipMemcpyFromSymbol(a.data(), HIP_SYMBOL(g_wtime), a.size() * 8) != hipSuccess ||
+        hipMemcpyFromSymbol(b.data(), HIP_SYMBOL(g_ftime), b.size() * 8) != hipSuccess)
+        return RVZ_EHIP;
+    for (int i = 0; i < n; ++i) {
+        for (int k = 0; k < 5; ++k) out[(size_t)i * 9 + k] = a[(size_t)i * 5 + k];
+        for (int k = 0; k < 4; ++k) out[(size_t)i * 9 + 5 + k] = b[(size_t)i * 4 + k];
+    }
+    std::vector<unsigned long long> z((size_t)WALK_STATS_MAX * 5, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtime), z.data(), z.size() * 8) != hipSuccess)
+        return RVZ_EHIP;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ftime), z.data(), (size_t)WALK_STATS_MAX * 4 * 8) ==
+                   hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 #endif
 

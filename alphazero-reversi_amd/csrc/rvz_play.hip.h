@@ -209,6 +209,8 @@ void k_play(PlayCtx ctx0) {
                 if (f & (PF_QUEUED | PF_DONE)) continue;
                 int k = __builtin_amdgcn_readfirstlane(st_k[j]);
                 int np = __builtin_amdgcn_readfirstlane(st_p[j]);
+                WT_NOW(ft_step);
+                FT_CNT();
                 for (;;) {
                     unsigned long long ab = 0;
                     if (k < E) {   // k_step: the pending expand + backup, then batch k's selection
@@ -223,11 +225,13 @@ void k_play(PlayCtx ctx0) {
                             carry = v.carry[g];
                         }
                         if (f & PF_READY) {
+                            WT_NOW(ft_e);
                             const ExpIn x = expand_load<BS>(v, g, lane, a.logits, a.value);
                             const int rn =
                                 expand_backup_phase<BS>(v, g, lane, x, 1, &root_meta, ab);
                             if (rn >= 0) root_n = rn;
                             f &= ~PF_READY;
+                            FT_ADD(0, ft_e);
                         }
                         const int bsz = min(a.B, a.S - k * a.B);
                         const int copies = select_phase<BS, float>(v, g, lane, first, bsz, k, root,
@@ -242,6 +246,7 @@ void k_play(PlayCtx ctx0) {
                         continue;
                     }
                     // k_act: the last batch's expand (or visit-count backup), the action, the move
+                    WT_NOW(ft_a);
                     bool over = false;
                     const int idx = act_game<BS>(v, g, lane, sp, (f & PF_READY) ? 1 : 2,
                                                  a.logits, 1, a.value, a.temperature, nullptr, 1,
@@ -263,6 +268,7 @@ void k_play(PlayCtx ctx0) {
                         sd = __shfl(sd, 0);
                         reset_game<BS>(v, g, lane, (uint32_t)(sd & 0xFFFFFFFFll), key);
                     }
+                    FT_ADD(1, ft_a);
                     ++np;
                     k = 0;
                     if (np >= task_plies) {
@@ -270,6 +276,7 @@ void k_play(PlayCtx ctx0) {
                         break;
                     }
                 }
+                FT_ADD(2, ft_step);
                 if (lane == 0) {
                     st_k[j] = k;
                     st_f[j] = f;
