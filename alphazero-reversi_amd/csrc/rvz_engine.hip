@@ -1715,7 +1715,7 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     if (e->BS == 8)
         return a->filters == 64 ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)
                                 : play_launch<128, 1, 2, 4, 8, 2>(e, v, pa, 2);
-    return a->filters == 64 ? play_launch<64, 4, 2, 5, 6, 1>(e, v, pa, 1)
+    return a->filters == 64 ? play_launch<64, 3, 2, 4, 6, 2>(e, v, pa, 2)
                             : play_launch<128, 1, 2, 3, 6, 2>(e, v, pa, 2);
 }
 

@@ -61,9 +61,17 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
         stamps += ((size_t)slot * gridDim.x + blockIdx.x) * 2;
     }
     // a compacted leaf batch (rvz_search_compact): dead boards are not evaluated, their rows are
-    // never read (uniform exit before the first barrier; NBOARD divides the stripe)
-    static_assert(RVZ_LIVE_STRIPE % NBOARD == 0, "stripe granule");
-    if (g0 >= n_boards || row_dead(n_live, g0)) {
+    // never read (a unit of dead boards exits before the first barrier; a unit across a stripe
+    // end (NBOARD not dividing the stripe) evaluates its live boards only)
+    int gb[NBOARD];
+    int n_eval = 0;
+#pragma unroll
+    for (int k = 0; k < NBOARD; ++k) {
+        const bool live = g0 + k < n_boards && !row_dead(n_live, g0 + k);
+        gb[k] = live ? g0 + k : -1;
+        n_eval += live ? 1 : 0;
+    }
+    if (n_eval == 0) {
         if (stamps && tid == 0) {
             stamps[0] = t_start;
             stamps[1] = __builtin_amdgcn_s_memrealtime() | stamp_xcc();
@@ -73,19 +81,13 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     PHASE(0);
     RT(0);
     HWID();
-    int gb[NBOARD];
-#pragma unroll
-    for (int k = 0; k < NBOARD; ++k) gb[k] = g0 + k < n_boards ? g0 + k : -1;
     h2_pass<F, NBOARD, CTW, PTW, BS>(smem, x, gb, nullptr, prm, L, blob, n_blocks,
                                      HeadsGlobalIdx<NBOARD>(work, gb), tid, lane, wave, ovf);
     PHASE(3);
     RT(1);
     if (ovf) work[(size_t)n_boards * 192] = 1.0f;   // benign race: every writer stores 1
     if (stamps) {   // end stamp; bits 56-63: the workgroup's live boards (bench.py's FLOPs)
-        const int rest = n_live ? n_live[g0 / RVZ_LIVE_STRIPE * RVZ_LIVE_PITCH] -
-                                      g0 % RVZ_LIVE_STRIPE
-                                : n_boards - g0;
-        const uint64_t nb = (uint64_t)(rest < NBOARD ? rest : NBOARD);
+        const uint64_t nb = (uint64_t)n_eval;
         __syncthreads();
         if (tid == 0) {
             stamps[0] = t_start;
@@ -166,8 +168,9 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
 #define RVZ_H2_DYN 1
 #endif
 #ifndef RVZ_H2_C5NB
-#define RVZ_H2_C5NB 4         // packed 6x6 at F = 64: boards per workgroup (4: 160 rows, 1 per CU;
-#endif                        // 2: 96 rows, two workgroups per CU)
+#define RVZ_H2_C5NB 3         // packed 6x6 at F = 64: boards per workgroup (3: 108 of 128 rows, two
+#endif                        // workgroups per CU, the 8x8 pair's tile map; 4: 160 rows, 1 per CU,
+                              // C5 -0.7%; 2: 96 rows, -12%)
 #ifndef RVZ_H2_SPARE
 #define RVZ_H2_SPARE 8        // 1/RVZ_H2_SPARE spare workgroups (a multiple of 8, at least 8)
 #endif
@@ -194,10 +197,10 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
 #ifndef RVZ_H2_DYN_LDS
 #define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
 #endif
-    if (BS == 6) {   // packed 6x6: F=64 4 boards = 160 pixel rows (10 tiles); F=128 1 board = 48
+    if (BS == 6) {   // packed 6x6: F=64 3 boards = 128 pixel rows (8 tiles); F=128 1 board = 48
         if (filters == 64)
-            hipLaunchKernelGGL((k_resnet_h2<64, RVZ_H2_C5NB, 2, RVZ_H2_C5NB == 4 ? 5 : 3, 6,
-                                            RVZ_H2_C5NB == 4 ? 1 : 2>), grid, dim3(256), 0, s, x, n,
+            hipLaunchKernelGGL((k_resnet_h2<64, RVZ_H2_C5NB, 2, (RVZ_H2_C5NB * 36 + 31) / 32,
+                                            6, RVZ_H2_C5NB == 4 ? 1 : 2>), grid, dim3(256), 0, s, x, n,
                                params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
                                claim);
         else

@@ -56,7 +56,8 @@ PRESETS = {   # BASELINE.json configs
     # per GPU, x8; a step = one self-play + training iteration (main_c4)
     "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, steps=1,
                warmup=0, fused=False),
-    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2, fused=False),
+    "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2, fused=True,
+               play_group=-24),
 }
 # measured beside the headline in the default N = 1 line (the largest single-GPU config and the
 # 6x6 variant); each is a full workload of its preset over the same --steps
@@ -112,7 +113,7 @@ def parse(argv=None):
     ap.add_argument("--fused", dest="fused", action="store_true", default=None,
                     help="the fused self-play launch (rvz_play): each workgroup plays its own "
                          "games, search + h2 evaluator + act + autoreset in one persistent kernel "
-                         "(the preset decides by default: C2 fused, C1/C3/C4/C5 not)")
+                         "(the preset decides by default: C2 and C5 fused, C1/C3/C4 not)")
     ap.add_argument("--no-fused", dest="fused", action="store_false",
                     help="the pull-style per-batch launches (k_step / trunk / heads per lane)")
     ap.add_argument("--play-group", type=int, default=None,
