@@ -30,6 +30,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -293,6 +294,33 @@ __device__ __forceinline__ ExpIn expand_load(const View& v, int g, int lane,
     return x;
 }
 
+// F.softmax(policy_logits, dim=1) over all S*S+1 outputs (mcts.py:596), one row per wave: lane
+// s < NSQ holds logit s, every lane the pass logit; returns (lane s's probability, 0 for lanes
+// >= NSQ; the pass probability). The expand's fused softmax and rvz_policy_softmax are this one
+// function (the expand uses .x only: no pass child is ever created).
+template <int NSQ>
+__device__ __forceinline__ float2 policy_softmax(float logit, float xpass, int lane) {
+    const float mx = fmaxf(wave_max_f(lane < NSQ ? logit : -INFINITY), xpass);
+    const float ex = lane < NSQ ? expf(logit - mx) : 0.0f;
+    const float ep = expf(xpass - mx);
+    const float denom = wave_sum_f(ex) + ep;
+    return make_float2(ex / denom, ep / denom);
+}
+
+// rvz_policy_softmax: one wave per row, WPB rows per workgroup
+template <int BS>
+__global__ __launch_bounds__(256) void k_policy_softmax(int n, const float* __restrict__ logits,
+                                                        float* __restrict__ probs) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * WPB + (threadIdx.x >> 6);
+    if (r >= n) return;
+    const float* row = logits + (size_t)r * NPOL;
+    const float2 p = policy_softmax<NSQ>(lane < NSQ ? row[lane] : 0.0f, row[NSQ], lane);
+    if (lane < NSQ) probs[(size_t)r * NPOL + lane] = p.x;
+    if (lane == 0) probs[(size_t)r * NPOL + NSQ] = p.y;
+}
+
 // expand + backup of the queued leaf: _process_batch pass 2 (mcts.py:600-623) and
 // MCTSNode.expand (:141-161). Returns the root's visit count after the backup (-1: nothing to
 // do) and, when the expanded leaf is the root, its new meta word in *root_meta.
@@ -307,12 +335,7 @@ __device__ __forceinline__ int expand_backup_phase(const View& v, int g, int lan
     Node* nodes = v.nodes + (size_t)g * v.M;
     uint32_t* meta = v.meta + (size_t)g * v.M;
     float prob = x.prob;
-    if (is_logits) {  // F.softmax(policy_logits, dim=1) over all S*S+1 outputs (mcts.py:596)
-        const float mx = fmaxf(wave_max_f(lane < NSQ ? prob : -INFINITY), x.xpass);
-        const float ex = lane < NSQ ? expf(prob - mx) : 0.0f;
-        const float denom = wave_sum_f(ex) + expf(x.xpass - mx);
-        prob = ex / denom;
-    }
+    if (is_logits) prob = policy_softmax<NSQ>(prob, x.xpass, lane).x;
     {   // non-finite NN output (any of the 65 probabilities or the value): device error word
         const bool bad = !__builtin_isfinite(x.val) || !__builtin_isfinite(x.xpass) ||
                          (lane < NSQ && !__builtin_isfinite(prob));
@@ -1085,6 +1108,25 @@ static int launch_check(rvz_engine* e, const char* what) {
 
 static int grid_games(int G) { return (G + WPB - 1) / WPB; }
 
+// Stream-ordered 32-bit fill as a kernel of our own instead of hipMemsetAsync: inside a captured
+// HIP graph a memset node's replays were seen to leave device words of the filled buffer
+// holding a 64-bit address (tools/diag_stagger.py: rvz_play's queue words after the second replay
+// of a 60-ply graph), after which the queue's task counter never reset. A kernel node has no
+// such problem, and costs one ~2 us launch.
+__global__ __launch_bounds__(256) void k_fill32(uint32_t* __restrict__ p, uint32_t v, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        p[i] = v;
+}
+
+static hipError_t fill32_async(void* p, uint32_t v, size_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(k_fill32, dim3((unsigned)blocks), dim3(256), 0, st,
+                       static_cast<uint32_t*>(p), v, n);
+    return hipGetLastError();
+}
+
 // Timing events: no system-scope fence (a fenced record writes back and invalidates the caches,
 // which would both slow the timed kernel and inflate the interval).
 static hipEvent_t timing_event(rvz_engine* e) {
@@ -1150,7 +1192,9 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
     e->NSQ = bs * bs;
     e->NPOL = e->NSQ + 1;
     e->E = E;
-    e->M = 1 + 2 * E * e->NSQ;   // root + two halves of E expansion blocks (the memo's two trees)
+    // root + E expansion blocks; rvz_search_memo(on) grows the pool to two halves of E blocks
+    // (the memo's two trees) the first time it is enabled, so memo-off engines hold one tree
+    e->M = 1 + E * e->NSQ;
     e->v.E = E;
     e->v.NS = (cfg->n_games + RVZ_LIVE_STRIPE - 1) / RVZ_LIVE_STRIPE;
     e->v.live = nullptr;
@@ -1283,7 +1327,7 @@ int rvz_env_get(rvz_engine* e, uint64_t* black, uint64_t* white, int32_t* status
 // (rvz_act with apply): a position set or moved from the host, or an abandoned search, drops them.
 static int memo_drop(rvz_engine* e) {
     if (!e->v.memo) return RVZ_OK;
-    RVZ_HIP(hipMemsetD32Async(e->v.carry, LINK_NONE, e->v.G, e->stream), e);
+    RVZ_HIP(fill32_async(e->v.carry, LINK_NONE, (size_t)e->v.G, e->stream), e);
     return RVZ_OK;
 }
 
@@ -1333,6 +1377,15 @@ int rvz_board_canonical(int32_t bs, int32_t n, const uint64_t* black, const uint
     return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
 }
 
+int rvz_policy_softmax(int32_t bs, int32_t n, const float* logits, float* probs, void* stream) {
+    if ((bs != 8 && bs != 6) || n < 0 || (n > 0 && (!logits || !probs))) return RVZ_EINVAL;
+    if (n == 0) return RVZ_OK;
+    dim3 grid((n + WPB - 1) / WPB), block(WPB * WAVE);
+    if (bs == 8) hipLaunchKernelGGL(k_policy_softmax<8>, grid, block, 0, (hipStream_t)stream, n, logits, probs);
+    else hipLaunchKernelGGL(k_policy_softmax<6>, grid, block, 0, (hipStream_t)stream, n, logits, probs);
+    return hipGetLastError() == hipSuccess ? RVZ_OK : RVZ_EHIP;
+}
+
 int rvz_env_legal(rvz_engine* e, uint64_t* out) {
     if (!e) return RVZ_EINVAL;
     int r = rvz_board_legal(e->BS, e->v.G, e->v.black, e->v.white, e->v.status, out, e->stream);
@@ -1359,8 +1412,8 @@ int rvz_search_begin(rvz_engine* e) {
     e->next_batch = 0;
     e->searching = 1;
     if (e->v.live && e->live_dirty) {   // an abandoned search left counts behind
-        RVZ_HIP(hipMemsetAsync(e->v.live, 0,
-                               sizeof(int32_t) * e->E * e->v.NS * RVZ_LIVE_PITCH, e->stream), e);
+        RVZ_HIP(fill32_async(e->v.live, 0u, (size_t)e->E * e->v.NS * RVZ_LIVE_PITCH, e->stream),
+                e);
         e->live_dirty = 0;
     }
     e->pending = 0;  // an unconsumed submit of an abandoned search is dropped
@@ -1457,11 +1510,44 @@ int rvz_search_compact(rvz_engine* e, int32_t on) {
     return RVZ_OK;
 }
 
+// The memo needs the node pool's second half (the previous search's tree stays readable while a
+// search writes the other half): the first rvz_search_memo(on) reallocates nodes and meta with
+// M = 1 + 2 E S^2. Outside a search no tree is live (the carried links are dropped here anyway),
+// so nothing is copied. Pointers held by an already captured graph would dangle: enable the memo
+// before capturing (rvz.Engine does it in its constructor).
+static int memo_grow(rvz_engine* e) {
+    const int M2 = 1 + 2 * e->E * e->NSQ;
+    if (e->M == M2) return RVZ_OK;
+    const size_t G = e->v.G;
+    Node* nodes = nullptr;
+    uint32_t* meta = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&nodes), G * M2 * sizeof(Node)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&meta), G * M2 * sizeof(uint32_t)) != hipSuccess) {
+        if (nodes) (void)hipFree(nodes);
+        e->err = "hipMalloc failed (the memo's second node-pool half)";
+        return RVZ_ENOMEM;
+    }
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);   // no launch may still read the old pool
+    for (void*& p : e->allocs) {
+        if (p == e->v.nodes) { (void)hipFree(p); p = nodes; }
+        else if (p == e->v.meta) { (void)hipFree(p); p = meta; }
+    }
+    e->v.nodes = nodes;
+    e->v.meta = meta;
+    e->M = e->v.M = M2;
+    RVZ_HIP(hipMemsetAsync(meta, 0, G * M2 * sizeof(uint32_t), e->stream), e);
+    return RVZ_OK;
+}
+
 int rvz_search_memo(rvz_engine* e, int32_t on) {
     if (!e) return RVZ_EINVAL;
     if (e->pending || (e->searching && e->next_batch > 0)) {
         e->err = "rvz_search_memo inside a search";
         return RVZ_EINVAL;
+    }
+    if (on) {
+        const int r = memo_grow(e);
+        if (r != RVZ_OK) return r;
     }
     e->v.memo = 1;             // so that memo_drop clears the links either way
     if (memo_drop(e) != RVZ_OK) return RVZ_EHIP;
@@ -1617,7 +1703,7 @@ static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slo
         if (a.gpw > play_gpw_max<F, BS>()) a.gpw = play_gpw_max<F, BS>();
         a.n_groups = (v.G + a.gpw - 1) / a.gpw;
         grid = dim3(a.n_groups < slots ? a.n_groups : slots);
-        RVZ_HIP(hipMemsetAsync(a.q_next, 0, sizeof(float) * play_qwords(v.G), e->stream), e);
+        RVZ_HIP(fill32_async(a.q_next, 0u, (size_t)play_qwords(v.G), e->stream), e);
     } else {            // static: workgroup w owns group w for every ply
         if (a.gpw <= 0) a.gpw = (v.G + slots - 1) / slots;
         if (a.gpw > play_gpw_max<F, BS>()) a.gpw = play_gpw_max<F, BS>();
@@ -1711,6 +1797,11 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.out_p = a->out_p;
     pa.hist = a->hist;
     pa.rows = reinterpret_cast<unsigned long long*>(a->rows_evaluated);
+    pa.budget = a->ply_budget;
+    // the queue's bounded wait (device error 16 when exceeded); RVZ_PLAY_SPIN_LIMIT lowers it to
+    // inject the timeout in tests (tests/test_gpu_play.py)
+    pa.spin_limit = 1u << 26;
+    if (const char* sl = getenv("RVZ_PLAY_SPIN_LIMIT")) pa.spin_limit = (unsigned)strtoul(sl, nullptr, 10);
     e->searching = 0;
     if (e->BS == 8)
         return a->filters == 64 ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)

@@ -38,6 +38,8 @@ struct PlayArgs {
     double* out_p;     // [G][NPOL] the last act's policy vector
     int32_t* hist;     // [plies][G] every act's index in this launch, or null
     unsigned long long* rows;   // += the rows this launch evaluated, or null
+    const int32_t* budget;      // [G] plies game g commits in this launch (<= plies), or null
+    unsigned spin_limit;        // queue waits give up (ERR_SCHED) after this many sleeps
     // schedule. Static (q_next null): workgroup w owns game group w for all `plies` plies.
     // Queue: tasks t = (group t % n_groups, ply t / n_groups) drawn in order from q_next; a
     // group's ply p starts after q_done[group] reached p (its ply p-1 published: agent-scope
@@ -152,21 +154,33 @@ void k_play(PlayCtx ctx0) {
         } else {
             PT_NOW(t_q0);
             if (tid == 0) {
-                const PlayArgs& a = play_ctx().a;
-                const unsigned t = __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT);
+                const PlayCtx& c = play_ctx();
+                const PlayArgs& a = c.a;
+                // once a wait timed out (ERR_SCHED) no workgroup draws another task: the launch
+                // drains, and the engine state is undefined until the games are reset (rvz.h)
+                const bool failed = __hip_atomic_load(c.v.err, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT) & ERR_SCHED;
+                const unsigned t =
+                    failed ? (unsigned)total
+                           : __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
                 int tg = -1, tp = 0;
                 if ((int)t < total) {
                     tg = (int)(t % (unsigned)a.n_groups);
                     tp = (int)(t / (unsigned)a.n_groups);
                     // the group's previous ply: played (and published) by the workgroup that
-                    // drew it n_groups tasks ago, which is running; bounded spin
+                    // drew it n_groups tasks ago, which is running; bounded spin, abandoned as
+                    // soon as another workgroup's wait timed out
                     unsigned spins = 0;
                     while ((int)__hip_atomic_load(a.q_done + tg, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT) < tp) {
                         __builtin_amdgcn_s_sleep(4);
-                        if (++spins > (1u << 26)) {
-                            atomicOr(play_ctx().v.err, ERR_SCHED);
+                        ++spins;
+                        if (spins > a.spin_limit ||
+                            ((spins & 1023u) == 0 &&
+                             (__hip_atomic_load(c.v.err, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) & ERR_SCHED))) {
+                            atomicOr(c.v.err, ERR_SCHED);
                             tg = -1;
                             break;
                         }
@@ -189,10 +203,13 @@ void k_play(PlayCtx ctx0) {
         const int g0 = gi * gpw;
         const int ng = min(gpw, G - g0);
         if (ng <= 0) break;
-        for (int j = tid; j < ng; j += 256) {
-            st_k[j] = 0;
-            st_f[j] = 0;
-            st_p[j] = 0;
+        {   // a game whose ply budget this task's ply reaches starts done
+            const int32_t* bud = play_ctx().a.budget;
+            for (int j = tid; j < ng; j += 256) {
+                st_k[j] = 0;
+                st_f[j] = (bud && ply0 >= bud[g0 + j]) ? PF_DONE : 0;
+                st_p[j] = 0;
+            }
         }
         __syncthreads();
         for (;;) {
@@ -271,7 +288,7 @@ void k_play(PlayCtx ctx0) {
                     FT_ADD(1, ft_a);
                     ++np;
                     k = 0;
-                    if (np >= task_plies) {
+                    if (np >= task_plies || (a.budget && ply0 + np >= a.budget[g])) {
                         f |= PF_DONE;
                         break;
                     }

@@ -11,7 +11,8 @@ Batched core:
     AlphaZeroNetwork, LeafEvaluator   the policy/value net at the evaluation boundary
 """
 from ._lib import RvzError, load  # noqa: F401
-from .engine import Engine, board_apply, board_canonical, board_legal  # noqa: F401
+from .engine import (Engine, board_apply, board_canonical, board_legal,  # noqa: F401
+                     policy_softmax)
 from .game import Board, ReversiGame  # noqa: F401
 from .mcts import MCTS  # noqa: F401
 from .network import AlphaZeroNetwork, LeafEvaluator, load_reference_state_dict  # noqa: F401

@@ -49,6 +49,7 @@ SIGNATURES = {
     "rvz_board_legal": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
     "rvz_board_apply": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P, _P, _P, _P]),
     "rvz_board_canonical": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P, _P, _P]),
+    "rvz_policy_softmax": (C.c_int, [C.c_int32, C.c_int32, _P, _P, _P]),
     "rvz_search_begin": (C.c_int, [_P]),
     "rvz_search_step": (C.c_int, [_P, _P, _P]),
     "rvz_search_submit": (C.c_int, [_P, _P, C.c_int32, _P]),
@@ -105,7 +106,8 @@ class PlayArgs(C.Structure):
                 ("games_per_workgroup", C.c_int32), ("temperature", C.c_double),
                 ("seeds", C.c_void_p), ("seed_stride", C.c_int64), ("plies_done", C.c_void_p),
                 ("games_done", C.c_void_p), ("out_idx", C.c_void_p), ("out_p", C.c_void_p),
-                ("hist", C.c_void_p), ("rows_evaluated", C.c_void_p)]
+                ("hist", C.c_void_p), ("rows_evaluated", C.c_void_p),
+                ("ply_budget", C.c_void_p)]
 
 
 def load() -> C.CDLL:

@@ -9,10 +9,11 @@ counterpart (mcts.py:220-226,446-542 only chunks one batch over local replicas s
 from __future__ import annotations
 
 import os
+import signal
 import socket
 import subprocess
 import time
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -71,35 +72,88 @@ def free_port() -> int:
     return port
 
 
-def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2) -> int:
+def visible_gpu_count() -> Optional[int]:
+    """GPUs this process may use, from the environment and sysfs only (no HIP call, so a launcher
+    parent stays uninitialised): the entries of HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES when set, else the KFD topology nodes with a GPU (nonzero
+    gfx_target_version). None when neither says."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = os.environ.get(var)
+        if val is not None:
+            return len([x for x in val.split(",") if x.strip() and x.strip() != "-1"])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(root)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(root, d, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    if k == "gfx_target_version" and int(v) != 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    return n
+
+
+def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2, kill_after_s: float = 10.0) -> int:
     """Run ``cmd`` as ``n`` rank processes on this node (one per GPU): each child gets RANK =
     LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = n and a shared 127.0.0.1 rendezvous, and
     inherits stdout/stderr. Children are separate processes started with Popen (never an exec of
     this one), so call this before anything touches the GPU. Returns 0 when every rank exits 0;
     otherwise the first failure's code (a signal maps to 1) after terminating the other ranks.
-    This is what `bench.py --gpus N` runs when no launcher (torchrun) set WORLD_SIZE."""
+    If the launcher itself is interrupted (KeyboardInterrupt, or SIGTERM, which is turned into
+    one here), every child still alive is terminated, then killed after ``kill_after_s``, so no
+    rank keeps holding a GPU or the rendezvous port. This is what `bench.py --gpus N` runs when
+    no launcher (torchrun) set WORLD_SIZE."""
     if n < 1:
         raise ValueError("need at least one rank")
     port = str(free_port())
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen(cmd, env=env))
-    rc, alive = 0, list(procs)
-    while alive:
-        for p in list(alive):
-            code = p.poll()
-            if code is None:
-                continue
-            alive.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                for q in alive:            # the exact children of this launcher, nothing else
-                    q.terminate()
-        if alive:
-            time.sleep(poll_s)
-    return rc
+
+    def on_term(signum, frame):
+        raise KeyboardInterrupt(f"signal {signum}")
+
+    try:
+        old = signal.signal(signal.SIGTERM, on_term)
+    except ValueError:                         # not the main thread: no handler, finally still runs
+        old = None
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            procs.append(subprocess.Popen(cmd, env=env))
+        rc, alive = 0, list(procs)
+        while alive:
+            for p in list(alive):
+                code = p.poll()
+                if code is None:
+                    continue
+                alive.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    for q in alive:            # the exact children of this launcher, nothing else
+                        q.terminate()
+            if alive:
+                time.sleep(poll_s)
+        return rc
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.terminate()
+        deadline = time.time() + kill_after_s
+        for p in live:
+            try:
+                p.wait(max(0.0, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        if old is not None:
+            signal.signal(signal.SIGTERM, old)
 
 
 def _device_for_backend():

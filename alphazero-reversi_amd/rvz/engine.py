@@ -211,15 +211,30 @@ class Engine:
         return ok
 
     # ------------------------------------------------------------------ fused self-play
+    def play_buffers(self, evaluator=None):
+        """Allocate what play() needs (the row counter, the launch scratch, the evaluator's
+        overflow word) outside any graph capture: allocated inside one, their zero-fill would be
+        recorded into the graph and every replay would reset the counter."""
+        if getattr(self, "play_rows", None) is None:   # rows evaluated by play() calls
+            self.play_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
+        n = self.lib.rvz_play_scratch_size(self._h)
+        sc = getattr(self, "_play_scratch", None)
+        if sc is None or sc.numel() < n:
+            self._play_scratch = torch.zeros(n, dtype=torch.float32, device=self.device)
+        if evaluator is not None and hasattr(evaluator, "ovf_word"):
+            evaluator.ovf_word()
+
     def play(self, evaluator, plies: int, temperature: float, seeds: torch.Tensor, stride: int,
              plies_done: torch.Tensor, games_done: torch.Tensor, reset: bool = True,
              skip_last_eval: bool = False, hist: Optional[torch.Tensor] = None,
-             games_per_workgroup: int = 0):
+             games_per_workgroup: int = 0, budget: Optional[torch.Tensor] = None):
         """rvz_play: every game commits `plies` plies (search of num_simulations + move + the
         autoreset bookkeeping of autoreset()) in ONE launch, the h2 LeafEvaluator's trunk and
         heads inside it; the same games, moves and counters as search() + act() + autoreset()
         with that evaluator (fused_softmax). idx_buf / p_buf: each game's last act. hist: int32
-        [plies, n_games] for every act's index, or None. Graph-capturable."""
+        [plies, n_games] for every act's index, or None. budget: int32 [n_games], game g commits
+        min(plies, budget[g]) plies (the others stay as they are), or None. Graph-capturable
+        once play_buffers() ran outside the capture (it runs here on the first eager call)."""
         from .network import LeafEvaluator
         if not isinstance(evaluator, LeafEvaluator):
             raise RvzError("play() runs the h2 LeafEvaluator inside the launch; another "
@@ -232,15 +247,21 @@ class Engine:
         if hist is not None and (hist.dtype != torch.int32 or hist.shape != (plies, self.n_games)
                                  or not hist.is_contiguous()):
             raise RvzError("play: hist int32 [plies, n_games]")
-        if getattr(self, "play_rows", None) is None:   # rows evaluated by play() calls
-            self.play_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
+        if budget is not None and (budget.dtype != torch.int32 or budget.numel() != self.n_games
+                                   or not budget.is_contiguous()
+                                   or budget.device != self.device):
+            raise RvzError("play: budget int32 [n_games] on the engine's device")
         n = self.lib.rvz_play_scratch_size(self._h)
-        sc = getattr(self, "_play_scratch", None)
-        if sc is None or sc.numel() < n:
-            sc = torch.zeros(n, dtype=torch.float32, device=self.device)
-            self._play_scratch = sc
-        if evaluator not in getattr(self, "_evaluators", ()):
-            self._evaluators = tuple(getattr(self, "_evaluators", ())) + (evaluator,)
+        ready = (getattr(self, "play_rows", None) is not None and
+                 getattr(self, "_play_scratch", None) is not None and
+                 self._play_scratch.numel() >= n and getattr(evaluator, "_ovf", None) is not None)
+        if not ready:
+            if torch.cuda.is_current_stream_capturing():
+                raise RvzError("play() inside a graph capture before its buffers exist: call "
+                               "Engine.play_buffers(evaluator) (or one eager play) first")
+            self.play_buffers(evaluator)
+        sc = self._play_scratch
+        self._bind(evaluator)
         a = _lib.PlayArgs(evaluator.params.data_ptr(), evaluator.wsplit.data_ptr(),
                           evaluator.filters, evaluator.n_blocks, sc.data_ptr(),
                           evaluator.ovf_word().data_ptr(), int(plies), int(bool(skip_last_eval)),
@@ -248,9 +269,20 @@ class Engine:
                           seeds.data_ptr(), int(stride), plies_done.data_ptr(),
                           games_done.data_ptr(), self.idx_buf.data_ptr(), self.p_buf.data_ptr(),
                           hist.data_ptr() if hist is not None else None,
-                          self.play_rows.data_ptr())
+                          self.play_rows.data_ptr(),
+                          budget.data_ptr() if budget is not None else None)
         self._stream()
         self._call("rvz_play", C.byref(a))
+
+    def _bind(self, evaluator):
+        """Remember the evaluator (check() reads its overflow word) and register this engine with
+        it: LeafEvaluator.refresh() (new weights) then drops this engine's memo links itself."""
+        evs = self.__dict__.setdefault("_evaluators", [])
+        if not any(e is evaluator for e in evs):
+            evs.append(evaluator)
+            reg = getattr(evaluator, "bind_engine", None)
+            if reg is not None:
+                reg(self)
 
     # ------------------------------------------------------------------ search
     def search_begin(self):
@@ -322,9 +354,7 @@ class Engine:
         fused_softmax=False applies torch's F.softmax (the reference's mcts.py:596) before the
         expand kernel instead of the kernel's fused softmax. skip_last_eval=True does not
         evaluate the last batch (rvz_search_skip; bit-identical visits, one NN call fewer)."""
-        evs = self.__dict__.setdefault("_evaluators", [])
-        if not any(e is evaluator for e in evs):
-            evs.append(evaluator)             # read by check()
+        self._bind(evaluator)
         self.search_begin()
         k = 0
         while self.search_step():
@@ -394,4 +424,18 @@ def board_canonical(black: torch.Tensor, white: torch.Tensor, status: torch.Tens
     out = torch.empty(n, 3, board_size, board_size, dtype=torch.float32, device=black.device)
     check(lib.rvz_board_canonical(board_size, n, ptr(black), ptr(white), ptr(status), ptr(out),
                                   _lib.stream_handle(black.device)), None, "rvz_board_canonical")
+    return out
+
+
+def policy_softmax(logits: torch.Tensor, board_size: int = 8) -> torch.Tensor:
+    """rvz_policy_softmax: F.softmax(logits, dim=1) (mcts.py:596) exactly as the engine's expand
+    computes it from logits (the fused softmax of search_submit(is_logits=True) and of play())."""
+    lib = _lib.load()
+    lg = logits.float().contiguous()
+    n = lg.shape[0]
+    if lg.shape != (n, board_size * board_size + 1):
+        raise RvzError(f"logits must be [n, {board_size * board_size + 1}]")
+    out = torch.empty_like(lg)
+    check(lib.rvz_policy_softmax(board_size, n, ptr(lg), ptr(out), _lib.stream_handle(lg.device)),
+          None, "rvz_policy_softmax")
     return out

@@ -191,13 +191,26 @@ class LeafEvaluator:
             self.params.data_ptr(), self.filters, self.n_blocks, self.wsplit.data_ptr(),
             _lib.stream_handle(self.device)), None, "rvz_resnet_h2_weights")
 
+    def bind_engine(self, engine):
+        """Called by an Engine the first time it searches or plays with this evaluator: refresh()
+        then drops that engine's NN-output memo (its carried outputs belong to the old net)."""
+        import weakref
+        eng = self.__dict__.setdefault("_engines", weakref.WeakSet())
+        eng.add(engine)
+
     @torch.no_grad()
     def refresh(self):
         """Re-read the module's (trained) weights and BN statistics into this evaluator's device
         buffers, in place: the addresses a captured HIP graph holds stay valid, so the next
-        replay evaluates the new net (the self-play / training loop, rvz.pipeline)."""
+        replay evaluates the new net (the self-play / training loop, rvz.pipeline). Every engine
+        that used this evaluator forgets its memo (Engine.memo_reset, stream-ordered after the
+        new weights): a memo link would otherwise hand the old net's priors and value to the
+        next search."""
         self.params.copy_(pack_resnet_params(self.net).to(self.device))
         self._h2_weights()
+        for eng in list(getattr(self, "_engines", ())):
+            if getattr(eng, "memo_on", False):
+                eng.memo_reset()
 
     def _forward_resnet(self, x: torch.Tensor, n_live=None):
         from . import _lib

@@ -87,8 +87,7 @@ class SelfPlayTrainer:
         self.trainer.sync_buffers()
         self.trainer.scheduler_step()          # pipeline.py:131, once per iteration
         self.model.eval()
-        self.evaluator.refresh()
-        self.eng.memo_reset()                  # the memo holds the previous net's outputs
+        self.evaluator.refresh()               # also drops the engine's memo (the old net's outputs)
         return out
 
     def run_iteration(self) -> Dict[str, float]:

@@ -67,6 +67,8 @@ class SelfPlayRunner:
             self.rec_p = torch.zeros(max_plies, G, engine.npol, dtype=torch.float64, device=dev)
             self.rec_over = torch.zeros(max_plies, G, 4, dtype=torch.int32, device=dev)
         self.ply_index = 0
+        if self.fused:       # play()'s buffers exist before any capture (Engine.play_buffers)
+            engine.play_buffers(evaluator)
 
     @property
     def steps(self) -> torch.Tensor:

@@ -131,6 +131,11 @@ def parse(argv=None):
     ap.add_argument("--sub-configs", default=None,
                     help="comma-separated presets measured beside the headline (default at one "
                          "rank with --config c2: c3,c5; 'none' for none)")
+    ap.add_argument("--no-stagger", action="store_true",
+                    help="start the timed window with every game at the same ply (all games begin "
+                         "together and stay in lockstep) instead of game g at ply g mod 60 of its "
+                         "game (one budgeted rvz_play launch before the warm-up): without the "
+                         "stagger a window shorter than a whole game measures one game phase")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
@@ -205,10 +210,13 @@ def launch(args):
     if "WORLD_SIZE" in os.environ or args.gpus <= 1:
         return
     from rvz import dist as rdist
+    # no torch.cuda call here: the parent never touches HIP before it starts the ranks (a device
+    # count can fall back to hipGetDeviceCount, i.e. initialise HIP in the parent); each rank's
+    # setup() refuses a LOCAL_RANK without a device
     if args.dist_backend == "nccl" and not args.dry_run:
-        avail = torch.cuda.device_count()     # counts devices without initialising HIP
-        if args.gpus > avail:
-            fail(f"--gpus {args.gpus} but only {avail} HIP device(s) visible (backend nccl)")
+        avail = rdist.visible_gpu_count()    # environment / sysfs only
+        if avail is not None and args.gpus > avail:
+            fail(f"--gpus {args.gpus} but only {avail} GPU(s) visible (backend nccl)")
     rc = rdist.spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:])
     sys.exit(rc)
 
@@ -255,6 +263,82 @@ def dry_run(args, rank, world, backend):
 
 
 # ------------------------------------------------------------------------------ measurement
+# every k_play dispatch this process makes (stagger, warm-up, timed, the --evals modes and the
+# sub-configs), timed with HIP events without system fence on its stream: the line's
+# k_play_dispatches, whose per-instantiation averages are what rocprofv3 --stats averages over
+# the same command (its timed subset is roofline.avg_ms_per_launch)
+DISPATCHES = []      # (kernel instantiation, label, ms)
+
+
+def play_kernel(board, filters):
+    """rvz_play's kernel instantiation for a geometry (csrc/rvz_engine.hip rvz_play)."""
+    return {(8, 64): "k_play<64, 2, 2, 4, 8, 2>", (8, 128): "k_play<128, 1, 2, 4, 8, 2>",
+            (6, 64): "k_play<64, 3, 2, 4, 6, 2>", (6, 128): "k_play<128, 1, 2, 3, 6, 2>"}[
+        (board, filters)]
+
+
+class Dispatches:
+    """HIP-event pairs around k_play dispatches on one stream, resolved after a synchronise."""
+
+    def __init__(self, kernel, device, n=512):
+        from rvz import _lib
+        self.kernel, self.timer, self.stream = kernel, _lib.Timer(2 * n), _lib.stream_handle(device)
+        self.marks = []
+
+    def __call__(self, label, fn):
+        a = self.timer.record(self.stream)
+        fn()
+        self.marks.append((label, a, self.timer.record(self.stream)))
+
+    def flush(self):
+        for label, a, b in self.marks:
+            DISPATCHES.append((self.kernel, label, self.timer.elapsed(a, b)))
+        self.marks = []
+
+
+def dispatch_summary():
+    out = {}
+    for k, label, ms in DISPATCHES:
+        d = out.setdefault(k, {"n": 0, "total_ms": 0.0, "by_label": {}})
+        d["n"] += 1
+        d["total_ms"] += ms
+        b = d["by_label"].setdefault(label, [0, 0.0])
+        b[0] += 1
+        b[1] += ms
+    for d in out.values():
+        d["avg_ms"] = round(d.pop("total_ms") / d["n"], 4)
+        d["by_label"] = {k: {"n": n, "avg_ms": round(t / n, 4)} for k, (n, t) in d["by_label"].items()}
+    return out or None
+
+
+def stagger(args, runners, tag, device):
+    """Phase-neutral start: every game begins at the start position together,
+    and 99.9% of 8x8 games last exactly 60 plies, so without this the games stay in lockstep and a
+    window of fewer than 60 plies samples one game phase. One rvz_play launch with per-game ply
+    budgets puts global game g at ply g mod L of its first game (L = S*S - 4 = 60 on 8x8, the
+    length of a full game): from then on every ply of the run holds a whole game's mix of
+    phases, as continuous self-play does (self_play.py:80-101). Runs on each lane's engine (the
+    pull-style presets continue from the state k_play leaves:
+    tests/test_gpu_play_oracle.py::test_stagger_then_pull_style_equals_fused). Returns the mean
+    plies per game it played."""
+    L = args.board * args.board - 4
+    disp = Dispatches(play_kernel(args.board, args.filters), device, n=len(runners))
+    tot, n = 0, 0
+    for r in runners:
+        bud = ((r.seeds - args.seed) % L).to(torch.int32).contiguous()   # global game index mod L
+        tot += int(bud.sum().item())
+        n += bud.numel()
+        disp(f"{tag}stagger", lambda r=r, bud=bud: r.eng.play(
+            r.evaluator, L - 1, r.temperature, r.seeds, r.seed_stride, r._plies, r._done,
+            reset=r.autoreset, skip_last_eval=r.skip_last_eval,
+            games_per_workgroup=getattr(r, "play_group", 0) if r.fused else 0, budget=bud))
+    torch.cuda.synchronize(device)
+    disp.flush()
+    for r in runners:
+        r.eng.check()
+    return tot / max(1, n)
+
+
 def make_net(args, device):
     import rvz
     torch.manual_seed(0)
@@ -524,6 +608,11 @@ def selfplay(args, device, rank, world, full=True):
         engines = [run.eng]
     eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
     run.start()
+    tag = "" if getattr(args, "label", None) is None else args.label + "."
+    stagger_plies = 0.0
+    if not args.no_stagger:
+        stagger_plies = stagger(args, [lane0] if args.fused else
+                                (run.runners if args.lanes > 1 else [run]), tag, device)
 
     # warmup: the first ply eager, then capture the ply graph with lane 0's trunk launches
     # stamping a ring of per-workgroup device wall-clock stamps, one row per launch (the heads
@@ -537,6 +626,7 @@ def selfplay(args, device, rank, world, full=True):
         raise SystemExit(f"--steps {args.steps} is not a multiple of --plies-per-graph {ppg}")
     cap_kw["plies"] = ppg
     warm = max(args.warmup, 0 if args.no_graph else 1)
+    wdisp = Dispatches(play_kernel(args.board, args.filters), device) if args.fused else None
     for i in range(warm):
         if i == 0 and not args.no_graph and not args.no_stamps and not args.fused:
             run.ply()
@@ -550,14 +640,20 @@ def selfplay(args, device, rank, world, full=True):
             ev.trunk_stamps = None
             continue
         if i == 0 and args.fused:
-            # a first launch of the same size as the timed one (so that every k_play dispatch of
-            # the run covers ppg plies: rocprofv3's average is then the timed launch's length)
-            run._body(ppg)
+            # a first launch of the same size as the timed one (every warm-up and timed k_play
+            # dispatch covers ppg plies)
+            wdisp(f"{tag}warmup", lambda: run._body(ppg))
+        elif args.fused:
+            wdisp(f"{tag}warmup", run.ply)
         else:
             run.ply()
         if i == 0 and not args.no_graph:
             run.capture(**cap_kw)
     torch.cuda.synchronize(device)
+    if wdisp is not None:
+        wdisp.flush()
+    # fused: every warm-up launch plays ppg plies; pull-style: one eager ply, then graph replays
+    warm_plies = warm * ppg if args.fused else (1 + (warm - 1) * ppg if warm else 0)
 
     def rows_now():
         if args.fused:
@@ -628,6 +724,7 @@ def selfplay(args, device, rank, world, full=True):
                      "lane running"}
     if ftimer is not None:
         durs = [ftimer.elapsed(2 * i, 2 * i + 1) for i in range(n_rep)]
+        DISPATCHES.extend((play_kernel(args.board, args.filters), f"{tag}timed", d) for d in durs)
         t_tr, rows_tr = sum(durs) / n_rep, rows / n_rep
         timing = (f"in the timed region: all {n_rep} k_play launches (one per graph replay, "
                   f"{ppg} plies each), HIP events without system fence around each replay on "
@@ -669,7 +766,13 @@ def selfplay(args, device, rank, world, full=True):
            # never waits for the host
            "host_enqueue_ms_per_step": round((t_enq[-1] - t0) / max(1, args.steps) * 1e3, 3),
            "plies_per_graph": ppg,
-           "play_group": args.play_group if args.fused else None}
+           "play_group": args.play_group if args.fused else None,
+           "warmup_plies": {"stagger_mean": round(stagger_plies, 2),
+                            "stagger": None if args.no_stagger else
+                            f"game g at ply g mod {args.board ** 2 - 4} of its game "
+                            "(one budgeted rvz_play launch)",
+                            "after_stagger": warm_plies,
+                            "total_mean": round(stagger_plies + warm_plies, 2)}}
     if full:
         kernels = {}
         for k in ("step", "act"):
@@ -711,6 +814,7 @@ def sub_config(base, name, device, rank, world):
         setattr(a, k, None)
     a.config = name
     a.stamps_dump = None
+    a.label = name
     apply_preset(a, name)
     r = selfplay(a, device, rank, world, full=False)
     out = {"value": round(r["value"], 2), "unit": "board-steps/s",
@@ -719,7 +823,7 @@ def sub_config(base, name, device, rank, world):
                        f"ResNet, {a.board}x{a.board}, {a.lanes} lane(s)",
            "games_per_gpu": a.games, "sims": a.sims, "nn": f"{a.blocks}x{a.filters}",
            "board": a.board, "lanes": a.lanes, "nn_rows_per_ply": r["nn_rows_per_ply"],
-           "roofline": r["roofline"]}
+           "warmup_plies": r["warmup_plies"], "roofline": r["roofline"]}
     del r
     torch.cuda.empty_cache()
     return out
@@ -869,6 +973,7 @@ def main():
             a = copy.copy(args)
             set_evals(a, mode)
             a.stamps_dump = None
+            a.label = f"evals_{mode}"
             o = selfplay(a, device, rank, world, full=False)
             evals_ab[mode] = {"value": round(o["value"], 2),
                               "ms_per_step": round(o["dt"] / args.steps * 1e3, 3),
@@ -897,6 +1002,7 @@ def main():
             "value": round(value, 2), "unit": "board-steps/s",
             "n_gpus": world, "rccl_world": tdist.get_world_size(), "dist_backend": backend,
             "steps": args.steps, "warmup": args.warmup,
+            "warmup_plies": r["warmup_plies"],
             "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "u64 rules + f32 NN (fp32 as 2-part f16 split on MFMA)",
@@ -930,6 +1036,7 @@ def main():
             "path_roofline": r["path_roofline"],
             "env_roofline": envb,
             "configs": subs or None,
+            "k_play_dispatches": dispatch_summary(),
             "cpu_baseline": cpu,
         }
         emit(out)

@@ -95,6 +95,12 @@ int rvz_board_canonical(int32_t board_size, int32_t n, const uint64_t *black,
                         const uint64_t *white, const int32_t *status, float *out,
                         void *hip_stream);
 
+/* F.softmax(policy_logits, dim=1) of _process_batch (mcts.py:596) over n rows of S*S+1 logits:
+ * bitwise the probabilities the expand computes when rvz_search_submit gets logits (is_logits = 1)
+ * and inside rvz_play (the same device function). The tests feed the oracle with it. */
+int rvz_policy_softmax(int32_t board_size, int32_t n, const float *logits, float *probs,
+                       void *hip_stream);
+
 /* ---- search (MCTS.search, mcts.py:322-407, one tree per game, lockstep over games) -------- */
 /* New root per live game from the engine's env state (mcts.py:334-341). */
 int rvz_search_begin(rvz_engine *e);
@@ -116,7 +122,9 @@ int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, con
  * discarded tree never reads (the leaf's children priors, W along the path; mcts.py:600-640), so
  * rvz_search_visits / rvz_act then back up the visit counts alone and return exactly the visits,
  * p and move of the evaluated search (tests/test_gpu_search.py::test_skip_last_eval_bit_exact).
- * An opt-in optimisation (one NN call fewer per move), not the reference's call sequence. */
+ * Off unless called (one NN call fewer per move; not the reference's call sequence). bench.py's
+ * headline uses it by default (--evals lazy: the memo + this, so the skipped evaluation is made
+ * later only if a search reaches that position; rvz_play's skip_last_eval is the same). */
 int rvz_search_skip(rvz_engine *e);
 /* Compacted leaf batches (on != 0; off by default): rvz_search_step writes the leaves that need an
  * evaluation (need[g] > 0; mcts.py:544-623 evaluates exactly those) to the first rows of their
@@ -139,6 +147,8 @@ const int32_t *rvz_search_live_count(const rvz_engine *e);
  * per-row net), and the net must not change between the two searches: call
  * rvz_search_memo_reset after new weights. Visits, p and moves are identical to the search
  * without the memo (tests/test_gpu_memo.py); it changes only how many rows are evaluated.
+ * The memo needs a second half of the node pool (the previous tree): the first call with on != 0
+ * reallocates the pool (device pointers change), so enable it before capturing a graph.
  * The carried links are dropped automatically by rvz_env_reset / rvz_env_autoreset (per game),
  * rvz_env_set, rvz_env_apply, rvz_act without apply and an abandoned search. Not inside a
  * search. */
@@ -190,7 +200,15 @@ typedef struct rvz_play_args {
     double *out_p;               /* float64 [n_games, S*S+1]: its policy vector */
     int32_t *hist;               /* int32 [plies][n_games]: every act's index, nullable */
     int64_t *rows_evaluated;     /* int64 [1] += the leaf rows evaluated by the call, nullable */
+    const int32_t *ply_budget;   /* int32 [n_games]: game g commits min(plies, ply_budget[g])
+                                    plies in this call (<= 0: none; it is left as it is), nullable
+                                    (every game commits `plies`). bench.py staggers the games'
+                                    phases with it (game g at ply g mod 60 of its game) */
 } rvz_play_args;
+/* A task-queue wait that times out (a workgroup waiting for its group's previous ply, bounded
+ * spin) sets device error bit 16 (rvz_check): the other workgroups then stop drawing tasks and the
+ * launch drains, leaving games at different ply counts. The engine state is then undefined until
+ * every game is reset (rvz_env_reset). */
 int64_t rvz_play_scratch_size(const rvz_engine *e);
 int rvz_play(rvz_engine *e, const rvz_play_args *a);
 

@@ -62,3 +62,77 @@ def test_spawn_ranks_propagates_a_failing_rank():
     assert spawn_ranks(3, [sys.executable, "-c", code]) == 3      # rank 2 is terminated
     ok = "import os; assert os.environ['MASTER_ADDR'] == '127.0.0.1'"
     assert spawn_ranks(2, [sys.executable, "-c", ok]) == 0
+
+
+def test_launcher_parent_never_touches_hip(monkeypatch):
+    """`bench.py --gpus N` (backend nccl) must start its ranks without any
+    torch.cuda call in the parent (a device count may initialise HIP through hipGetDeviceCount,
+    and a HIP-initialised parent must not fork the rank processes)."""
+    import torch
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "alphazero-reversi_amd"))
+    import bench
+    from rvz import dist as rdist
+
+    def refuse(*a, **k):
+        raise AssertionError("the launcher parent called into torch.cuda")
+
+    for name in ("device_count", "is_available", "init", "_lazy_init", "current_device",
+                 "set_device", "synchronize"):
+        monkeypatch.setattr(torch.cuda, name, refuse)
+    started = []
+    monkeypatch.setattr(rdist, "spawn_ranks", lambda n, cmd: started.append((n, cmd)) or 0)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5,6,7")
+    args = bench.parse(["--gpus", "8", "--dist-backend", "nccl"])
+    with pytest.raises(SystemExit) as ex:
+        bench.launch(args)
+    assert ex.value.code == 0 and started and started[0][0] == 8
+    assert not torch.cuda.is_initialized()
+    # more ranks than visible GPUs: refused from the environment alone, still without HIP
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    with pytest.raises(SystemExit) as ex:
+        bench.launch(bench.parse(["--gpus", "4"]))
+    assert ex.value.code == 2 and len(started) == 1
+    assert not torch.cuda.is_initialized()
+
+
+def test_visible_gpu_count_from_environment(monkeypatch):
+    sys.path.insert(0, os.path.join(ROOT, "alphazero-reversi_amd"))
+    from rvz.dist import visible_gpu_count
+    for v in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "3,5")
+    assert visible_gpu_count() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert visible_gpu_count() == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    n = visible_gpu_count()                      # sysfs (no GPU in this container: 0 or None)
+    assert n is None or n >= 0
+
+
+def test_spawn_ranks_terminates_children_when_the_launcher_is_killed(tmp_path):
+    """a SIGTERM to the launcher must not leave rank processes holding GPUs or the
+    rendezvous port."""
+    import signal
+    import time
+    pkg = os.path.join(ROOT, "alphazero-reversi_amd")
+    child = ("import os, time; open(os.path.join(%r, 'pid%%s' %% os.environ['RANK']), 'w')"
+             ".write(str(os.getpid())); time.sleep(120)" % str(tmp_path))
+    launcher = ("import sys; sys.path.insert(0, %r); from rvz.dist import spawn_ranks; "
+                "sys.exit(spawn_ranks(2, [sys.executable, '-c', %r], kill_after_s=5))"
+                % (pkg, child))
+    p = subprocess.Popen([sys.executable, "-c", launcher], env=_env())
+    pids = []
+    t0 = time.time()
+    while len(pids) < 2 and time.time() - t0 < 60:
+        pids = [int(f.read_text()) for f in tmp_path.glob("pid*") if f.read_text()]
+        time.sleep(0.1)
+    assert len(pids) == 2, "ranks did not start"
+    p.send_signal(signal.SIGTERM)
+    p.wait(timeout=60)
+    for pid in pids:
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)

@@ -133,3 +133,78 @@ def _ddp_vs_plain(socket, dist, rvz, DDPTrainer):
     ddp = min(diff(sd[i], sd[3]) for i in range(3))
     assert moved > 1e-3                       # the nets trained
     assert ddp <= 4 * noise + 1e-6 * moved, (ddp, noise, moved)
+
+
+@pytest.mark.timeout(900)
+def test_c4_per_rank_shard_over_rccl_world1(oracle):
+    """C4's per-rank shard as configured (BASELINE.json configs[3]: 32,768 games x 800 sims per
+    GPU, 10x128 net): one SelfPlayTrainer iteration (whole games, records ->
+    training arrays, 100 DDP steps whose gradients go through RCCL at world 1, evaluator refresh),
+    then the next iteration's self-play. 16 sampled games of that iteration are replayed by the
+    literal oracle fed the TRAINED net's h2 outputs (reference pipeline.py:114-150 plays the new
+    iteration with the updated model): every ply's move and f64 policy, and their rows of the
+    training arrays (states, policy_targets, value_targets; self_play.py:117-126)."""
+    import socket
+    import torch.distributed as dist
+    import rvz
+    from oracle_play import OracleGames
+    from rvz.pipeline import SelfPlayTrainer
+    G, S, seed = 32768, 800, 11
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        net = rvz.AlphaZeroNetwork(8, 10, 128).cuda()
+        init = {k: v.clone() for k, v in net.state_dict().items()}
+        spt = SelfPlayTrainer(net, G, num_simulations=S, seed=seed, train_steps=100,
+                              train_batch=64)
+        assert spt.distributed and spt.world == 1
+        r0 = spt.run_iteration()
+        assert r0["board_steps"] == r0["samples"] >= 59 * G and r0["steps"] == 100
+        assert np.isfinite(r0["train/loss"])
+        moved = max((net.state_dict()[k].float() - init[k].float()).abs().max().item()
+                    for k in init if init[k].is_floating_point())
+        assert moved > 1e-4
+        data = spt.generate()                   # iteration 1: the trained net, graph replays
+    finally:
+        dist.destroy_process_group()
+    run = spt.runner
+    rec_idx = run.rec_idx.cpu().numpy()
+    counts = (rec_idx >= 0).sum(0)
+    assert int(counts.sum()) == data["states"].shape[0]
+    first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    sample = np.linspace(0, G - 1, 16).astype(int)
+    orc = OracleGames(oracle, [seed + G + int(g) for g in sample], S)
+    ev = spt.evaluator                          # refreshed in place: the trained weights
+    ev_fresh = rvz.LeafEvaluator(net.eval())
+    x = (torch.rand(64, 3, 8, 8, device="cuda") > 0.6).float()
+    assert all(torch.equal(a, b) for a, b in zip(ev(x), ev_fresh(x)))
+    states = data["states"].cpu().numpy()
+    pol = data["policy_targets"].cpu().numpy()
+    val = data["value_targets"].cpu().numpy().reshape(-1)
+    rec_p = run.rec_p.cpu().numpy()
+    sides = []
+    for ply in range(spt.max_plies):
+        if orc.over():
+            break
+        live = np.array([not g.over for g in orc.games])
+        sd = [g.side for g in orc.games]
+        _, oi, op, planes = orc.ply(ev)
+        for j, g in enumerate(sample):
+            if not live[j]:
+                continue
+            assert oi[j] == rec_idx[ply, g], (ply, g)
+            assert np.array_equal(op[j].view(np.int64), rec_p[ply, g].view(np.int64)), (ply, g)
+            row = first[g] + ply
+            assert np.array_equal(states[row], planes[j]), (ply, g)
+            assert np.array_equal(pol[row], op[j].astype(np.float32)), (ply, g)
+            sides.append((row, sd[j], j))
+    assert orc.over()
+    for j, g in enumerate(sample):
+        assert counts[g] == sum(1 for r, _, jj in sides if jj == j)
+    win = orc.winners()
+    for row, side, j in sides:
+        want = 0.0 if win[j] == 0 else (1.0 if side == win[j] else -1.0)
+        assert val[row] == want, (row, side, win[j])
