@@ -1083,6 +1083,13 @@ struct rvz_engine {
     std::vector<std::pair<int, size_t>> ev_marks;  // (kind 0 = k_step, 1 = k_act, first event)
     std::vector<void*> allocs;
     std::string err;
+    // rvz_play_table: the cross-game NN-output table (tab null: off)
+    unsigned long long* tab = nullptr;
+    unsigned* tclaim = nullptr;
+    unsigned* tgen = nullptr;
+    int64_t tslots = 0;
+    int tmaxd = 0;
+    const void* tab_blob = nullptr;   // the weight blob the current generation's rows came from
 };
 
 static thread_local std::string g_create_error;
@@ -1116,6 +1123,28 @@ static int grid_games(int G) { return (G + WPB - 1) / WPB; }
 __global__ __launch_bounds__(256) void k_fill32(uint32_t* __restrict__ p, uint32_t v, size_t n) {
     for (size_t i = blockIdx.x * (size_t)256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
         p[i] = v;
+}
+
+// a new table generation (new weights): every slot of an older generation reads as empty
+__global__ void k_table_bump(unsigned* gen) {
+    if (threadIdx.x == 0) atomicAdd(gen, 1u);
+}
+
+static int table_bump(rvz_engine* e) {
+    if (!e->tgen) return RVZ_OK;
+    hipLaunchKernelGGL(k_table_bump, dim3(1), dim3(64), 0, e->stream, e->tgen);
+    RVZ_HIP(hipGetLastError(), e);
+    return RVZ_OK;
+}
+
+static void table_free(rvz_engine* e) {
+    for (void* p : {(void*)e->tab, (void*)e->tclaim, (void*)e->tgen})
+        if (p) (void)hipFree(p);
+    e->tab = nullptr;
+    e->tclaim = nullptr;
+    e->tgen = nullptr;
+    e->tslots = 0;
+    e->tab_blob = nullptr;
 }
 
 static hipError_t fill32_async(void* p, uint32_t v, size_t n, hipStream_t st) {
@@ -1257,6 +1286,7 @@ int rvz_create(const rvz_config* cfg, rvz_engine** out) {
 
 void rvz_destroy(rvz_engine* e) {
     if (!e) return;
+    table_free(e);
     for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
     for (void* p : e->allocs)
         if (p) (void)hipFree(p);
@@ -1557,7 +1587,44 @@ int rvz_search_memo(rvz_engine* e, int32_t on) {
 
 int rvz_search_memo_reset(rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
-    return memo_drop(e);
+    const int r = memo_drop(e);
+    return r != RVZ_OK ? r : table_bump(e);   // new weights: the table's rows are stale too
+}
+
+int rvz_play_table(rvz_engine* e, int64_t slots, int32_t max_discs) {
+    if (!e) return RVZ_EINVAL;
+    if (slots != 0 && (slots < 1024 || (slots & (slots - 1)) != 0 || slots > (1ll << 30) ||
+                       max_discs < 4)) {
+        e->err = "rvz_play_table: slots a power of two in [1024, 2^30] (or 0), max_discs >= 4";
+        return RVZ_EINVAL;
+    }
+    RVZ_HIP(hipStreamSynchronize(e->stream), e);
+    if (slots == e->tslots && slots != 0) {   // same size: new limit, a fresh generation
+        e->tmaxd = max_discs;
+        return table_bump(e);
+    }
+    table_free(e);
+    if (slots == 0) return RVZ_OK;
+    const size_t stride = e->BS == 8 ? TabGeo<8>::STRIDE : TabGeo<6>::STRIDE;
+    if (hipMalloc(reinterpret_cast<void**>(&e->tab), (size_t)slots * stride * 8) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&e->tclaim), (size_t)slots * 4) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&e->tgen), 4) != hipSuccess) {
+        table_free(e);
+        e->err = "hipMalloc failed (rvz_play_table)";
+        return RVZ_ENOMEM;
+    }
+    hipError_t st = hipMemset(e->tab, 0, (size_t)slots * stride * 8);   // tags 0: no generation
+    if (st == hipSuccess) st = hipMemset(e->tclaim, 0, (size_t)slots * 4);
+    if (st == hipSuccess) st = hipMemsetD32(e->tgen, 1u, 1);
+    if (st == hipSuccess) st = hipDeviceSynchronize();
+    if (st != hipSuccess) {
+        table_free(e);
+        e->err = std::string("rvz_play_table init: ") + hipGetErrorString(st);
+        return RVZ_EHIP;
+    }
+    e->tslots = slots;
+    e->tmaxd = max_discs;
+    return RVZ_OK;
 }
 
 int rvz_search_rows_total(rvz_engine* e, int64_t* out) {
@@ -1798,6 +1865,26 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.hist = a->hist;
     pa.rows = reinterpret_cast<unsigned long long*>(a->rows_evaluated);
     pa.budget = a->ply_budget;
+    pa.tab = nullptr;
+    pa.tclaim = nullptr;
+    pa.tgen = nullptr;
+    pa.tmask = 0;
+    pa.tmaxd = 0;
+    pa.tstats = reinterpret_cast<unsigned long long*>(a->table_stats);
+    if (e->tab) {
+        if (e->tab_blob != a->blob) {   // other weights than the generation's rows came from
+            if (e->tab_blob) {
+                const int r = table_bump(e);
+                if (r != RVZ_OK) return r;
+            }
+            e->tab_blob = a->blob;
+        }
+        pa.tab = e->tab;
+        pa.tclaim = e->tclaim;
+        pa.tgen = e->tgen;
+        pa.tmask = (unsigned)(e->tslots - 1);
+        pa.tmaxd = e->tmaxd;
+    }
     // the queue's bounded wait (device error 16 when exceeded); RVZ_PLAY_SPIN_LIMIT lowers it to
     // inject the timeout in tests (tests/test_gpu_play.py)
     pa.spin_limit = 1u << 26;

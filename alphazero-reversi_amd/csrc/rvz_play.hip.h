@@ -40,6 +40,13 @@ struct PlayArgs {
     unsigned long long* rows;   // += the rows this launch evaluated, or null
     const int32_t* budget;      // [G] plies game g commits in this launch (<= plies), or null
     unsigned spin_limit;        // queue waits give up (ERR_SCHED) after this many sleeps
+    // the cross-game NN-output table (rvz_play_table; tab null: off)
+    unsigned long long* tab;    // [slots][TabGeo<BS>::STRIDE] granules {value, tag = generation}
+    unsigned* tclaim;           // [slots] the generation that claimed the slot
+    const unsigned* tgen;       // the current generation (device word, >= 1)
+    unsigned tmask;             // slots - 1
+    int tmaxd;                  // positions with at most this many discs are looked up / stored
+    unsigned long long* tstats; // += {hits, inserts}, or null
     // schedule. Static (q_next null): workgroup w owns game group w for all `plies` plies.
     // Queue: tasks t = (group t % n_groups, ply t / n_groups) drawn in order from q_next; a
     // group's ply p starts after q_done[group] reached p (its ply p-1 published: agent-scope
@@ -61,6 +68,157 @@ __host__ __device__ constexpr int play_gpw_max() {
 // its row in this cycle's passes, its row held back last cycle (an odd row waits one cycle)
 enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4, PF_EVAL = 8, PF_HELD = 16 };
 constexpr int32_t ERR_SCHED = 16;   // a queue wait timed out (device error word)
+
+// ---- the cross-game NN-output table (rvz_play_table) ---------------------------------------
+// An h2 row's outputs depend only on its input planes (test_h2_live_rows), and the planes are a
+// function of three bitboards (mover, opponent, the mover's legal moves: get_canonical_state,
+// game.py:131-162). So a row evaluated once — by any game, in any earlier cycle, with the same
+// weights — can stand in for a new evaluation of the same (P, O, V): its logits and value are
+// bitwise what the trunk and heads would return. The opening positions repeat across games
+// (tools/exp_xgame.py: 11.9% of the C2 headline's rows repeat an earlier row's position).
+// Slot layout: NG = NSQ + 8 granules of 8 bytes {32-bit datum, 32-bit tag}: logits 0..NSQ-1, the
+// pass logit (NSQ), the value (NSQ + 1), the key words P lo/hi, O lo/hi, V lo/hi (NSQ + 2 ..).
+// Every granule is stored whole by one agent-scope 8-byte store and read by agent-scope 8-byte
+// loads (MI355X_MICROARCH.md R2 granules: the data is its own flag, no fence): a reader accepts
+// a slot only if every granule carries the current generation as its tag and the key matches;
+// a slot being written, empty, or of an older generation fails the tag check (a miss, never a
+// wrong row). A slot is claimed once per generation by a compare-and-swap of its claim word, so
+// all granules tagged with a generation were written by that generation's one claimant; a new
+// generation (new weights: rvz_search_memo_reset, or another weight blob) invalidates every slot
+// without touching the table.
+template <int BS>
+struct TabGeo {
+    static constexpr int NSQ = Geo<BS>::NSQ;
+    static constexpr int NG = NSQ + 8;
+    static constexpr int STRIDE = (NG + 7) / 8 * 8;   // granules per slot (64-byte multiple)
+};
+constexpr int TAB_PROBES = 8;
+
+__device__ __forceinline__ uint64_t tab_mix(uint64_t z) {
+    z ^= z >> 30;
+    z *= 0xbf58476d1ce4e5b9ull;
+    z ^= z >> 27;
+    z *= 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t tab_hash(uint64_t P, uint64_t O, uint64_t V) {
+    return tab_mix(P ^ tab_mix(O ^ tab_mix(V + 0x9e3779b97f4a7c15ull)));
+}
+// the datum of granule idx of a slot holding (P, O, V) with this row / value (key part only
+// when row is null)
+template <int NSQ>
+__device__ __forceinline__ uint32_t tab_key_word(int idx, uint64_t P, uint64_t O, uint64_t V) {
+    const int k = idx - (NSQ + 2);
+    const uint64_t w = k < 2 ? P : (k < 4 ? O : V);
+    return (k & 1) ? (uint32_t)(w >> 32) : (uint32_t)w;
+}
+
+// Loads slot `sl`'s granules (lane l: granules l and 64 + l) and checks tags and key: returns
+// 0 if some granule is not of generation `gen` (empty, being written, older), 1 if the slot is a
+// whole slot of this generation holding another key, 2 if it holds (P, O, V).
+template <int BS>
+__device__ __forceinline__ int tab_read(const unsigned long long* __restrict__ tab, uint32_t sl,
+                                         uint32_t gen, uint64_t P, uint64_t O, uint64_t V,
+                                         int lane, uint64_t& x0, uint64_t& x1) {
+    using T = TabGeo<BS>;
+    constexpr int NSQ = T::NSQ, NG = T::NG;
+    const unsigned long long* e = tab + (size_t)sl * T::STRIDE;
+    x0 = 0;
+    x1 = 0;
+    if (lane < NG) x0 = __hip_atomic_load(e + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (NG > 64 && lane < NG - 64)
+        x1 = __hip_atomic_load(e + 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool stale = false, other = false;
+    if (lane < NG) {
+        stale |= (uint32_t)(x0 >> 32) != gen;
+        if (lane >= NSQ + 2) other |= (uint32_t)x0 != tab_key_word<NSQ>(lane, P, O, V);
+    }
+    if (NG > 64 && lane < NG - 64) {
+        stale |= (uint32_t)(x1 >> 32) != gen;
+        if (64 + lane >= NSQ + 2) other |= (uint32_t)x1 != tab_key_word<NSQ>(64 + lane, P, O, V);
+    }
+    if (__ballot(stale) != 0ull) return 0;
+    return __ballot(other) != 0ull ? 1 : 2;
+}
+
+// granule idx's datum, wave-uniform (idx a compile-time constant >= NSQ)
+template <int BS, int IDX>
+__device__ __forceinline__ uint32_t tab_datum(uint64_t x0, uint64_t x1) {
+    if constexpr (IDX < 64) return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x0, IDX);
+    else return (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x1, IDX - 64);
+}
+
+// A hit writes the stored row into the game's logits / value rows (as the FC heads would) and
+// returns true. Probes stop at the first slot that is not a valid slot of this generation.
+template <int BS>
+__device__ __forceinline__ bool tab_lookup(const PlayArgs& a, uint32_t gen, uint64_t P,
+                                           uint64_t O, uint64_t V, int lane, int g) {
+    constexpr int NSQ = Geo<BS>::NSQ, NPOL = Geo<BS>::NPOL;
+    const uint64_t h = tab_hash(P, O, V);
+    for (int i = 0; i < TAB_PROBES; ++i) {
+        const uint32_t sl = (uint32_t)(h + i) & a.tmask;
+        uint64_t x0, x1;
+        const int r = tab_read<BS>(a.tab, sl, gen, P, O, V, lane, x0, x1);
+        if (r == 0) return false;   // not a whole slot of this generation: the chain ends
+        if (r == 1) continue;       // another key's slot: probe on
+        float* row = a.logits + (size_t)g * NPOL;
+        if (lane < NSQ) row[lane] = __uint_as_float((uint32_t)x0);
+        if (lane == 0) {
+            row[NSQ] = __uint_as_float(tab_datum<BS, NSQ>(x0, x1));
+            a.value[g] = __uint_as_float(tab_datum<BS, NSQ + 1>(x0, x1));
+        }
+        return true;
+    }
+    return false;
+}
+
+// Stores game g's evaluated row (a.logits / a.value, written by the FC heads of this
+// workgroup) for (P, O, V). Returns 1 if this wave wrote a slot.
+template <int BS>
+__device__ __forceinline__ int tab_insert(const PlayArgs& a, uint32_t gen, uint64_t P, uint64_t O,
+                                          uint64_t V, int lane, int g) {
+    using T = TabGeo<BS>;
+    constexpr int NSQ = T::NSQ, NPOL = Geo<BS>::NPOL, NG = T::NG;
+    const uint64_t h = tab_hash(P, O, V);
+    for (int i = 0; i < TAB_PROBES; ++i) {
+        const uint32_t sl = (uint32_t)(h + i) & a.tmask;
+        uint32_t c = 0;
+        if (lane == 0) c = __hip_atomic_load(a.tclaim + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+        if (c == gen) {   // taken in this generation: ours already, or another key's
+            uint64_t x0, x1;
+            if (tab_read<BS>(a.tab, sl, gen, P, O, V, lane, x0, x1) == 2) return 0;
+            continue;
+        }
+        uint32_t won = 0;
+        if (lane == 0) {
+            uint32_t expect = c;
+            won = __hip_atomic_compare_exchange_strong(a.tclaim + sl, &expect, gen,
+                                                       __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) ? 1u : 0u;
+        }
+        if (!__builtin_amdgcn_readfirstlane((int)won)) continue;
+        const float* row = a.logits + (size_t)g * NPOL;
+        const float val = a.value[g];
+        unsigned long long* e = a.tab + (size_t)sl * T::STRIDE;
+        const unsigned long long tag = (unsigned long long)gen << 32;
+        if (lane < NG) {
+            const uint32_t d = lane < NPOL ? __float_as_uint(row[lane])
+                               : lane == NSQ + 1 ? __float_as_uint(val)
+                                                 : tab_key_word<NSQ>(lane, P, O, V);
+            __hip_atomic_store(e + lane, tag | d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (NG > 64 && lane < NG - 64) {
+            const int idx = 64 + lane;
+            const uint32_t d = idx < NPOL ? __float_as_uint(row[idx])
+                               : idx == NSQ + 1 ? __float_as_uint(val)
+                                                : tab_key_word<NSQ>(idx, P, O, V);
+            __hip_atomic_store(e + idx, tag | d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return 1;
+    }
+    return 0;
+}
 
 struct PlayCtx {
     View v;
@@ -127,6 +285,7 @@ void k_play(PlayCtx ctx0) {
     __shared__ int s_nq;
     __shared__ float vpart[4][16];
     __shared__ int s_task[2];
+    __shared__ unsigned s_tgen;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int E, G, gpw, total, queue, task_plies;
@@ -141,6 +300,11 @@ void k_play(PlayCtx ctx0) {
     }
     bool ovf = false;
     int n_rows = 0;                      // rows this workgroup evaluated
+    unsigned n_hits = 0, n_ins = 0;      // table hits (per wave) / inserts
+    if (tid == 0) {
+        const PlayArgs& a = play_ctx().a;
+        s_tgen = a.tab ? __hip_atomic_load(a.tgen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    }
     double* sp = reinterpret_cast<double*>(smem) + wave * (NPOL + 7);
     uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
     PT_NOW(t_start);
@@ -257,6 +421,19 @@ void k_play(PlayCtx ctx0) {
                         ++k;
                         // the last batch's row with skip_last: left unevaluated (rvz_search_skip)
                         if (copies > 0 && !(k == E && a.skip_last)) {
+                            if (a.tab) {   // an earlier evaluation of this position: no new row
+                                const uint64_t P = st_bits[3 * j], O = st_bits[3 * j + 1],
+                                               Vb = st_bits[3 * j + 2];
+                                if (__popcll(P | O) <= a.tmaxd &&
+                                    tab_lookup<BS>(a, s_tgen, P, O, Vb, lane, g)) {
+                                    // the expand reads the row (and select's pend / path words)
+                                    // back in this wave
+                                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+                                    f |= PF_READY;
+                                    ++n_hits;
+                                    continue;
+                                }
+                            }
                             f |= PF_QUEUED;
                             break;
                         }
@@ -372,6 +549,15 @@ void k_play(PlayCtx ctx0) {
                         a.work, HeadRowsList{q_rows + h0}, a.prm, a.L, a.logits, a.value,
                         reinterpret_cast<float*>(smem), vpart, opaque_tid());
             }
+            if (play_ctx().a.tab) {   // store the new rows of table positions (one wave per row)
+                __syncthreads();      // the heads' logits / value rows are written
+                for (int i = wave; i < nq; i += WPB) {
+                    const PlayArgs& a = play_ctx().a;
+                    const uint64_t P = q_bits[3 * i], O = q_bits[3 * i + 1], Vb = q_bits[3 * i + 2];
+                    if (__popcll(P | O) <= a.tmaxd)
+                        n_ins += tab_insert<BS>(a, s_tgen, P, O, Vb, opaque_tid() & 63, q_rows[i]);
+                }
+            }
             for (int j = tid; j < ng; j += 256)
                 if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
             __syncthreads();
@@ -405,4 +591,9 @@ void k_play(PlayCtx ctx0) {
     if (ovf && ovw) *ovw = 1.0f;   // benign race: every writer stores 1
     unsigned long long* rows = play_ctx().a.rows;
     if (rows && tid == 0) atomicAdd(rows, (unsigned long long)n_rows);
+    unsigned long long* ts = play_ctx().a.tstats;
+    if (ts && (tid & 63) == 0) {   // per wave: its hits and inserts
+        if (n_hits) atomicAdd(ts, (unsigned long long)n_hits);
+        if (n_ins) atomicAdd(ts + 1, (unsigned long long)n_ins);
+    }
 }

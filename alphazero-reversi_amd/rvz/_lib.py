@@ -75,6 +75,7 @@ SIGNATURES = {
     "rvz_act": (C.c_int, [_P, C.c_double, _P, C.c_int32, _P, _P]),
     "rvz_play_scratch_size": (C.c_int64, [_P]),
     "rvz_play": (C.c_int, [_P, _P]),
+    "rvz_play_table": (C.c_int, [_P, C.c_int64, C.c_int32]),
     "rvz_counters": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "rvz_stats_enable": (C.c_int, [_P, C.c_int32]),
     "rvz_stats_read": (C.c_int, [_P, C.POINTER(C.c_int64)]),
@@ -107,7 +108,7 @@ class PlayArgs(C.Structure):
                 ("seeds", C.c_void_p), ("seed_stride", C.c_int64), ("plies_done", C.c_void_p),
                 ("games_done", C.c_void_p), ("out_idx", C.c_void_p), ("out_p", C.c_void_p),
                 ("hist", C.c_void_p), ("rows_evaluated", C.c_void_p),
-                ("ply_budget", C.c_void_p)]
+                ("ply_budget", C.c_void_p), ("table_stats", C.c_void_p)]
 
 
 def load() -> C.CDLL:

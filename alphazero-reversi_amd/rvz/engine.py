@@ -217,6 +217,8 @@ class Engine:
         recorded into the graph and every replay would reset the counter."""
         if getattr(self, "play_rows", None) is None:   # rows evaluated by play() calls
             self.play_rows = torch.zeros(1, dtype=torch.int64, device=self.device)
+            # {table hits, table inserts} of play() calls (rvz_play_table)
+            self.table_stats = torch.zeros(2, dtype=torch.int64, device=self.device)
         n = self.lib.rvz_play_scratch_size(self._h)
         sc = getattr(self, "_play_scratch", None)
         if sc is None or sc.numel() < n:
@@ -270,7 +272,8 @@ class Engine:
                           games_done.data_ptr(), self.idx_buf.data_ptr(), self.p_buf.data_ptr(),
                           hist.data_ptr() if hist is not None else None,
                           self.play_rows.data_ptr(),
-                          budget.data_ptr() if budget is not None else None)
+                          budget.data_ptr() if budget is not None else None,
+                          self.table_stats.data_ptr())
         self._stream()
         self._call("rvz_play", C.byref(a))
 
@@ -283,6 +286,16 @@ class Engine:
             reg = getattr(evaluator, "bind_engine", None)
             if reg is not None:
                 reg(self)
+
+    def table(self, slots: int = 1 << 20, max_discs: int = 14):
+        """rvz_play_table: the cross-game NN-output table of play() (slots = 0: off). A leaf whose
+        position has at most max_discs discs takes the logits and value an earlier evaluation of
+        the same position stored (any game of this engine, same weights): the same games, fewer
+        evaluated rows. New weights: memo_reset() / LeafEvaluator.refresh() start a new
+        generation. Call before capturing a graph."""
+        self._stream()
+        self._call("rvz_play_table", int(slots), int(max_discs))
+        self.table_slots = int(slots)
 
     # ------------------------------------------------------------------ search
     def search_begin(self):

@@ -209,8 +209,8 @@ class LeafEvaluator:
         self.params.copy_(pack_resnet_params(self.net).to(self.device))
         self._h2_weights()
         for eng in list(getattr(self, "_engines", ())):
-            if getattr(eng, "memo_on", False):
-                eng.memo_reset()
+            if getattr(eng, "memo_on", False) or getattr(eng, "table_slots", 0):
+                eng.memo_reset()                  # also a new generation of the play() table
 
     def _forward_resnet(self, x: torch.Tensor, n_live=None):
         from . import _lib

@@ -82,14 +82,21 @@ def parse(argv=None):
     ap.add_argument("--board", type=int, default=None)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--instrument-plies", type=int, default=2)
-    ap.add_argument("--evals", choices=("lazy", "memo", "reference"), default="lazy",
-                    help="which NN rows are evaluated (the games are bit-identical in all three, "
-                         "tests/test_gpu_memo.py): 'reference' = every leaf of every batch, as the "
-                         "reference does (it rebuilds the tree every move, mcts.py:334); 'memo' = "
-                         "a leaf the game's previous search already evaluated takes that output "
-                         "(rvz_search_memo); 'lazy' = memo, and each search's last batch is left "
-                         "unevaluated (rvz_search_skip: nothing reads its output in that search) "
-                         "and evaluated by a later search only if one reaches its position")
+    ap.add_argument("--evals", choices=("table", "lazy", "memo", "reference"), default="table",
+                    help="which NN rows are evaluated (the games are bit-identical in all four, "
+                         "tests/test_gpu_memo.py, tests/test_gpu_table.py): 'reference' = every "
+                         "leaf of every batch, as the reference does (it rebuilds the tree every "
+                         "move, mcts.py:334); 'memo' = a leaf the game's previous search already "
+                         "evaluated takes that output (rvz_search_memo); 'lazy' = memo, and each "
+                         "search's last batch is left unevaluated (rvz_search_skip: nothing reads "
+                         "its output in that search) and evaluated by a later search only if one "
+                         "reaches its position; 'table' = lazy, and (fused launch only) an opening "
+                         "position any game evaluated before takes the stored output "
+                         "(rvz_play_table)")
+    ap.add_argument("--table-slots", type=int, default=1 << 20,
+                    help="--evals table: slots of the cross-game NN-output table (power of two)")
+    ap.add_argument("--table-discs", type=int, default=14,
+                    help="--evals table: positions with at most this many discs use the table")
     ap.add_argument("--skip-last-eval", action="store_true",
                     help="leave each search's last batch unevaluated (also without the memo)")
     ap.add_argument("--no-memo", action="store_true",
@@ -165,7 +172,8 @@ def set_evals(args, mode):
     """--evals mode -> the engine switches (skip_last_eval stays on if asked for explicitly)."""
     args.evals = mode
     args.no_memo = mode == "reference"
-    args.skip_last_eval = mode == "lazy" or getattr(args, "force_skip", False)
+    args.skip_last_eval = mode in ("lazy", "table") or getattr(args, "force_skip", False)
+    args.table = mode == "table"
 
 
 def apply_preset(args, name):
@@ -576,8 +584,11 @@ def selfplay(args, device, rank, world, full=True):
         return rvz.LeafEvaluator(net, device=device)
 
     def make_eng(n):
-        return rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
-                          compact_leaves=not args.no_compact, memo=not args.no_memo)
+        e = rvz.Engine(n, args.sims, args.batch, 1.0, board_size=args.board, device=device,
+                       compact_leaves=not args.no_compact, memo=not args.no_memo)
+        if args.table and args.fused:      # the table serves rvz_play (the fused launch) only
+            e.table(args.table_slots, args.table_discs)
+        return e
 
     first_game = rank * args.games          # global game index space: rank r owns a shard
     if args.fused:
@@ -661,6 +672,7 @@ def selfplay(args, device, rank, world, full=True):
         return sum(e.rows_total() for e in engines)
 
     rows0 = rows_now()
+    tab0 = eng.table_stats.clone() if args.fused else None
     if graph_events:
         graph_events[1].zero_()            # the ring starts with the timed region
     rdist.barrier()
@@ -689,6 +701,7 @@ def selfplay(args, device, rank, world, full=True):
     rdist.barrier()
     s1 = int(run.steps.item())
     rows1 = rows_now()
+    tab_d = (eng.table_stats - tab0).tolist() if tab0 is not None else None
     for e in engines:
         e.check()
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
@@ -761,6 +774,10 @@ def selfplay(args, device, rank, world, full=True):
     out = {"value": value, "dt": dt, "total": total, "roofline": roof, "net": net,
            "eng": eng, "ev": ev, "lanes": args.lanes,
            "nn_rows_per_ply": round(rows / max(1, plies_local), 3),
+           "table": ({"slots": args.table_slots, "max_discs": args.table_discs,
+                      "hits_per_ply": round(tab_d[0] / max(1, plies_local), 3),
+                      "inserts_per_ply": round(tab_d[1] / max(1, plies_local), 3)}
+                     if tab_d is not None and args.table else None),
            "nn_calls_per_ply": sum(calls_per_search),
            # host time to enqueue the timed plies (graph replays): below ms_per_step, the device
            # never waits for the host
@@ -967,7 +984,7 @@ def main():
         # the same workload with the other --evals modes: the games are identical
         # (tests/test_gpu_memo.py, test_bench_configuration_at_full_size_plays_the_plain_games), so
         # the row differences are the memo's hits and the deferred last batches
-        for mode in ("reference", "memo", "lazy"):
+        for mode in ("reference", "memo", "lazy", "table"):
             if mode == args.evals:
                 continue
             a = copy.copy(args)
@@ -1020,8 +1037,11 @@ def main():
                        if args.lanes > 1 else None,
                        "evals": args.evals, "skip_last_eval": args.skip_last_eval,
                        "memo": not args.no_memo,
+                       "table": ({"slots": args.table_slots, "max_discs": args.table_discs}
+                                 if args.table and args.fused else None),
                        "parallelism": f"games sharded x{world}"},
             "nn_rows_per_ply": r["nn_rows_per_ply"],
+            "table": r["table"],
             "nn_calls_per_ply": r["nn_calls_per_ply"],
             "host_enqueue_ms_per_step": r["host_enqueue_ms_per_step"],
             "evals_ab": evals_ab or None,

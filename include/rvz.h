@@ -204,6 +204,7 @@ typedef struct rvz_play_args {
                                     plies in this call (<= 0: none; it is left as it is), nullable
                                     (every game commits `plies`). bench.py staggers the games'
                                     phases with it (game g at ply g mod 60 of its game) */
+    int64_t *table_stats;        /* int64 [2] += {table hits, table inserts} (rvz_play_table), nullable */
 } rvz_play_args;
 /* A task-queue wait that times out (a workgroup waiting for its group's previous ply, bounded
  * spin) sets device error bit 16 (rvz_check): the other workgroups then stop drawing tasks and the
@@ -211,6 +212,20 @@ typedef struct rvz_play_args {
  * every game is reset (rvz_env_reset). */
 int64_t rvz_play_scratch_size(const rvz_engine *e);
 int rvz_play(rvz_engine *e, const rvz_play_args *a);
+/* Cross-game NN-output table for rvz_play (off by default; slots = 0 turns it off and frees it).
+ * The reference evaluates every leaf (mcts.py:544-623) and carries an inert transposition table
+ * for reuse (mcts.py:228-320, 368-385); here, a leaf whose position (mover, opponent, legal-move
+ * bitboards: exactly the NN input planes, game.py:131-162) has at most max_discs discs is looked
+ * up in a device hash table of `slots` entries (a power of two) before it is queued, and an
+ * evaluated row of such a position is stored: a hit expands the leaf from the stored logits and
+ * value, which are bitwise what the h2 evaluator returns for that position (its row outputs depend
+ * only on the row: tests/test_gpu_network.py), from any earlier evaluation by any game of the
+ * engine. Visits, p and moves are identical with and without it (tests/test_gpu_table.py); it
+ * changes how many rows are evaluated. Like the memo it requires unchanged weights:
+ * rvz_search_memo_reset (new weights in place) starts a new table generation, and so does a call
+ * of rvz_play with another weight blob. 8-byte {datum, generation} granules written and read with
+ * agent-scope accesses, so workgroups on every XCD share it without fences. Not inside a search. */
+int rvz_play_table(rvz_engine *e, int64_t slots, int32_t max_discs);
 
 /* ---- introspection (tests / bench) -------------------------------------------------------- */
 /* Stream-ordered HIP event timer, events without system fence (the engine's own launch timing

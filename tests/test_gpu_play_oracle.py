@@ -25,9 +25,11 @@ def _net(board, blocks, filters, seed=0):
     return rvz.AlphaZeroNetwork(board, blocks, filters).cuda().eval()
 
 
-def _fused_runner(net, G, S, memo=True, skip=True, seed_base=42, gpw=0):
+def _fused_runner(net, G, S, memo=True, skip=True, seed_base=42, gpw=0, table=None):
     import rvz
     eng = rvz.Engine(G, S, 64, board_size=net.board_size, memo=memo)
+    if table:
+        eng.table(*table)
     run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=seed_base,
                              skip_last_eval=skip, fused=True)
     run.play_group = gpw
@@ -44,8 +46,8 @@ def _play(run, plies, budget=None):
     return hist
 
 
-def _vs_oracle(oracle, net, G, S, plies, gpw, sample_n=16, memo=True, skip=True):
-    run = _fused_runner(net, G, S, memo=memo, skip=skip, gpw=gpw)
+def _vs_oracle(oracle, net, G, S, plies, gpw, sample_n=16, memo=True, skip=True, table=None):
+    run = _fused_runner(net, G, S, memo=memo, skip=skip, gpw=gpw, table=table)
     sample = np.linspace(0, G - 1, sample_n).astype(int)
     orc = OracleGames(oracle, [42 + int(g) for g in sample], S, bs=net.board_size)
     compared = 0
@@ -67,10 +69,12 @@ def _vs_oracle(oracle, net, G, S, plies, gpw, sample_n=16, memo=True, skip=True)
 
 def test_k_play_c2_headline_form_vs_oracle(oracle):
     """bench.py's C2 headline form at full size: 4,096 games x 800 sims, the 6x64 net, memo and
-    the last batch left to it (--evals lazy), the task queue with groups of 6 (play_group -6);
-    16 sampled games, 3 plies, each ply one k_play launch."""
+    the last batch left to it, the cross-game table (--evals table), the task queue with groups
+    of 6 (play_group -6); 16 sampled games, 3 plies, each ply one k_play launch. In these plies
+    every game's leaves are opening positions that other games evaluated: table hits."""
     net = _net(8, 6, 64)
-    _vs_oracle(oracle, net, 4096, 800, 3, -6)
+    run = _vs_oracle(oracle, net, 4096, 800, 3, -6, table=(1 << 20, 14))
+    assert int(run.eng.table_stats[0].item()) > 0
 
 
 def test_k_play_c5_preset_vs_oracle(oracle):
@@ -78,7 +82,7 @@ def test_k_play_c5_preset_vs_oracle(oracle):
     boards (three per workgroup), groups of 24; 16 sampled games, 2 plies (parity of the 6x6
     variant is unpinned by design: the reference's Board rejects size != 8, board.py:27-28)."""
     net = _net(6, 6, 64)
-    _vs_oracle(oracle, net, 16384, 400, 2, -24)
+    _vs_oracle(oracle, net, 16384, 400, 2, -24, table=(1 << 20, 14))
 
 
 def test_k_play_c3_shape_vs_oracle_whole_games(oracle):
