@@ -52,7 +52,8 @@ PRESETS = {   # BASELINE.json configs
     # LDS: one workgroup per CU, nothing covers the search phases) the launches are faster
     "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2, fused=True,
                play_group=-6),
-    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, fused=False),
+    "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, fused=True,
+               play_group=-16),
     # per GPU, x8; a step = one self-play + training iteration (main_c4)
     "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, steps=1,
                warmup=0, fused=False),

@@ -23,10 +23,16 @@ blocks, filters = (int(x) for x in os.environ.get("NET", "6x64").split("x"))
 torch.manual_seed(0)
 net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
 eng = rvz.Engine(G, S, 64, memo=True)
+if int(os.environ.get("TABLE", 1)):        # bench.py's default --evals table
+    eng.table(1 << 20, 14)
 run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=42,
                          skip_last_eval=True, fused=True)
 run.play_group = int(os.environ.get("GROUP", -6))
 run.start()
+if int(os.environ.get("STAGGER", 1)):      # bench.py's phase stagger: game g at ply g mod 60
+    bud = ((run.seeds - 42) % 60).to(torch.int32).contiguous()
+    eng.play(run.evaluator, 59, 1.0, run.seeds, run.seed_stride, run._plies, run._done,
+             reset=True, skip_last_eval=True, games_per_workgroup=run.play_group, budget=bud)
 lib = rvz.load()
 lib.rvz_play_timing_read.argtypes = [C.c_void_p, C.c_int]
 n_wg = 16384
