@@ -552,9 +552,11 @@ def cpu_baseline(args, net):
             "env_tree_only_1core": one}
 
 
-def stored_traffic(args, kernel):
+def stored_traffic(args, kernel, plies=None):
     """HBM bytes per launch of `kernel` from the committed PMC passes (--pmc), quoted only for the
-    configuration they were measured on (C2, 4,096 games), with their source named."""
+    configuration they were measured on (C2, 4,096 games), with their source named. k_play: the
+    passes' launches cover `plies_per_launch` plies; a launch of another length gets the bytes
+    scaled by its plies, and the label says so."""
     if not (os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096):
         return None, None
     try:
@@ -566,6 +568,10 @@ def stored_traffic(args, kernel):
         return None, None
     src = (f"{os.path.relpath(args.pmc, ROOT)} ({pmc.get('source', 'stored rocprofv3 PMC passes')}"
            "; not measured in this run)")
+    pl = pmc.get(kernel, {}).get("plies_per_launch")
+    if plies and pl and plies != pl:
+        b = round(b * plies / pl)
+        src += f"; scaled from {pl}-ply to {plies}-ply launches"
     return b, src
 
 
@@ -752,7 +758,8 @@ def selfplay(args, device, rank, world, full=True):
     ach = fpr * rows_tr / (t_tr * 1e-3) / 1e12
     ach_u = upr * rows_tr / (t_tr * 1e-3) / 1e12
     region = fpr * rows / (t1 - t0) / 1e12      # every lane's evaluated rows / timed wall time
-    traffic, traffic_src = (stored_traffic(args, "play" if args.fused else "nn_trunk")
+    traffic, traffic_src = (stored_traffic(args, "play" if args.fused else "nn_trunk",
+                                           ppg if args.fused else None)
                             if full else (None, None))
     roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma",
             "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
