@@ -848,7 +848,7 @@ def sub_config(base, name, device, rank, world):
                        f"ResNet, {a.board}x{a.board}, {a.lanes} lane(s)",
            "games_per_gpu": a.games, "sims": a.sims, "nn": f"{a.blocks}x{a.filters}",
            "board": a.board, "lanes": a.lanes, "nn_rows_per_ply": r["nn_rows_per_ply"],
-           "warmup_plies": r["warmup_plies"], "roofline": r["roofline"]}
+           "warmup_plies": r["warmup_plies"], "table": r["table"], "roofline": r["roofline"]}
     del r
     torch.cuda.empty_cache()
     return out
