@@ -1871,6 +1871,15 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.tmask = 0;
     pa.tmaxd = 0;
     pa.tstats = reinterpret_cast<unsigned long long*>(a->table_stats);
+    pa.rec_black = a->rec_black;
+    pa.rec_white = a->rec_white;
+    pa.rec_side = a->rec_side;
+    pa.rec_p = a->rec_p;
+    if ((a->rec_black || a->rec_white || a->rec_side || a->rec_p) &&
+        !(a->rec_black && a->rec_white && a->rec_side && a->rec_p)) {
+        e->err = "rvz_play: rec_black, rec_white, rec_side and rec_p go together";
+        return RVZ_EINVAL;
+    }
     if (e->tab) {
         if (e->tab_blob != a->blob) {   // other weights than the generation's rows came from
             if (e->tab_blob) {

@@ -47,6 +47,12 @@ struct PlayArgs {
     unsigned tmask;             // slots - 1
     int tmaxd;                  // positions with at most this many discs are looked up / stored
     unsigned long long* tstats; // += {hits, inserts}, or null
+    // self-play records (or null): the position before each committed act and its policy vector,
+    // [plies][G] (rec_p [plies][G][NPOL]); hist holds the act's index
+    uint64_t* rec_black;
+    uint64_t* rec_white;
+    int32_t* rec_side;
+    double* rec_p;
     // schedule. Static (q_next null): workgroup w owns game group w for all `plies` plies.
     // Queue: tasks t = (group t % n_groups, ply t / n_groups) drawn in order from q_next; a
     // group's ply p starts after q_done[group] reached p (its ply p-1 published: agent-scope
@@ -442,9 +448,19 @@ void k_play(PlayCtx ctx0) {
                     // k_act: the last batch's expand (or visit-count backup), the action, the move
                     WT_NOW(ft_a);
                     bool over = false;
+                    double* outp = a.out_p;
+                    if (a.rec_black) {   // the record of this ply: the position before the move
+                        const size_t ri = (size_t)(ply0 + np) * v.G + g;
+                        if (lane == 0) {
+                            a.rec_black[ri] = v.black[g];
+                            a.rec_white[ri] = v.white[g];
+                            a.rec_side[ri] = v.status[(size_t)g * 4];
+                        }
+                        outp = a.rec_p + (size_t)(ply0 + np) * v.G * Geo<BS>::NPOL;
+                    }
                     const int idx = act_game<BS>(v, g, lane, sp, (f & PF_READY) ? 1 : 2,
                                                  a.logits, 1, a.value, a.temperature, nullptr, 1,
-                                                 a.out_idx, a.out_p, &over);
+                                                 a.out_idx, outp, &over);
                     f &= ~PF_READY;
                     // k_autoreset: count the ply; a finished game restarts with its slot's next
                     // seed

@@ -108,7 +108,9 @@ class PlayArgs(C.Structure):
                 ("seeds", C.c_void_p), ("seed_stride", C.c_int64), ("plies_done", C.c_void_p),
                 ("games_done", C.c_void_p), ("out_idx", C.c_void_p), ("out_p", C.c_void_p),
                 ("hist", C.c_void_p), ("rows_evaluated", C.c_void_p),
-                ("ply_budget", C.c_void_p), ("table_stats", C.c_void_p)]
+                ("ply_budget", C.c_void_p), ("table_stats", C.c_void_p),
+                ("rec_black", C.c_void_p), ("rec_white", C.c_void_p), ("rec_side", C.c_void_p),
+                ("rec_p", C.c_void_p)]
 
 
 def load() -> C.CDLL:

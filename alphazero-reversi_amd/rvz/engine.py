@@ -229,14 +229,18 @@ class Engine:
     def play(self, evaluator, plies: int, temperature: float, seeds: torch.Tensor, stride: int,
              plies_done: torch.Tensor, games_done: torch.Tensor, reset: bool = True,
              skip_last_eval: bool = False, hist: Optional[torch.Tensor] = None,
-             games_per_workgroup: int = 0, budget: Optional[torch.Tensor] = None):
+             games_per_workgroup: int = 0, budget: Optional[torch.Tensor] = None,
+             records=None):
         """rvz_play: every game commits `plies` plies (search of num_simulations + move + the
         autoreset bookkeeping of autoreset()) in ONE launch, the h2 LeafEvaluator's trunk and
         heads inside it; the same games, moves and counters as search() + act() + autoreset()
         with that evaluator (fused_softmax). idx_buf / p_buf: each game's last act. hist: int32
         [plies, n_games] for every act's index, or None. budget: int32 [n_games], game g commits
-        min(plies, budget[g]) plies (the others stay as they are), or None. Graph-capturable
-        once play_buffers() ran outside the capture (it runs here on the first eager call)."""
+        min(plies, budget[g]) plies (the others stay as they are), or None. records: (black
+        int64 [plies, G], white int64 [plies, G], side int32 [plies, G], p float64
+        [plies, G, npol]): the position before every act and its policy vector (hist: the move;
+        p_buf is then not written), or None. Graph-capturable once play_buffers() ran outside
+        the capture (it runs here on the first eager call)."""
         from .network import LeafEvaluator
         if not isinstance(evaluator, LeafEvaluator):
             raise RvzError("play() runs the h2 LeafEvaluator inside the launch; another "
@@ -253,6 +257,18 @@ class Engine:
                                    or not budget.is_contiguous()
                                    or budget.device != self.device):
             raise RvzError("play: budget int32 [n_games] on the engine's device")
+        rec = (None,) * 4
+        if records is not None:
+            rb, rw, rs, rp = records
+            G = self.n_games
+            if not (rb.dtype == rw.dtype == torch.int64 and rs.dtype == torch.int32
+                    and rp.dtype == torch.float64 and rb.shape == rw.shape == rs.shape
+                    == (plies, G) and rp.shape == (plies, G, self.npol)
+                    and all(t.is_contiguous() and t.device == self.device
+                            for t in (rb, rw, rs, rp))):
+                raise RvzError("play: records = (black int64, white int64 [plies, G], side int32 "
+                               "[plies, G], p float64 [plies, G, npol]) on the engine's device")
+            rec = tuple(t.data_ptr() for t in records)
         n = self.lib.rvz_play_scratch_size(self._h)
         ready = (getattr(self, "play_rows", None) is not None and
                  getattr(self, "_play_scratch", None) is not None and
@@ -273,7 +289,7 @@ class Engine:
                           hist.data_ptr() if hist is not None else None,
                           self.play_rows.data_ptr(),
                           budget.data_ptr() if budget is not None else None,
-                          self.table_stats.data_ptr())
+                          self.table_stats.data_ptr(), *rec)
         self._stream()
         self._call("rvz_play", C.byref(a))
 

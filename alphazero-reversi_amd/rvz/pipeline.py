@@ -36,7 +36,8 @@ class SelfPlayTrainer:
                  train_steps: Optional[int] = None, train_batch: int = 64, lr: float = 1e-3,
                  weight_decay: float = 1e-4, gradient_clip: float = 1.0,
                  graph: bool = True, compact_leaves: bool = True, lr_milestones=(),
-                 lr_gamma: float = 0.1, memo: bool = True):
+                 lr_gamma: float = 0.1, memo: bool = True, fused: bool = True,
+                 table_slots: int = 1 << 20, table_discs: int = 14):
         self.model = model.eval()
         self.device = next(model.parameters()).device
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -52,9 +53,16 @@ class SelfPlayTrainer:
         self.eng = Engine(games, num_simulations, batch_size, c_puct, board_size=bs,
                           device=self.device, compact_leaves=compact_leaves, memo=memo)
         self.max_plies = bs * bs - 4
+        # fused: every game of the iteration in ONE rvz_play launch with device records, the
+        # memo's deferred last batch and the cross-game table (a new generation per refresh());
+        # else the pull-style ply graph (per-batch launches, records copied per ply)
+        self.fused = bool(fused)
+        if self.fused and table_slots:
+            self.eng.table(table_slots, table_discs)
         self.runner = SelfPlayRunner(self.eng, self.evaluator, temperature, record=True,
                                      max_plies=self.max_plies,
-                                     seed_base=self.seed + self.rank * self.games)
+                                     seed_base=self.seed + self.rank * self.games,
+                                     fused=self.fused, skip_last_eval=self.fused and memo)
         self.graph = bool(graph)
         self.iteration = 0
 
@@ -69,10 +77,13 @@ class SelfPlayTrainer:
         run = self.runner
         self._seeds()
         run.start()
-        for k in range(self.max_plies):
-            if self.graph and run.graph is None and k == 1:
-                run.capture()                   # after one eager ply (kernel warm-up)
-            run.ply()
+        if self.fused:
+            run.play_record(self.max_plies)     # one launch: whole games, records on the device
+        else:
+            for k in range(self.max_plies):
+                if self.graph and run.graph is None and k == 1:
+                    run.capture()               # after one eager ply (kernel warm-up)
+                run.ply()
         run.check()
         if not bool(run.post_status[:, 1].all()):
             raise RuntimeError(f"a game is not over after {self.max_plies} plies")

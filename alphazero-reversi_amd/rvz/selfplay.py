@@ -36,8 +36,10 @@ class SelfPlayRunner:
         # act + autoreset per workgroup) instead of the per-batch launches; same games
         self.fused = bool(fused)
         self.play_group = 0       # Engine.play's games_per_workgroup (0: the task queue default)
-        if self.fused and (record or not fused_softmax):
-            raise ValueError("the fused runner plays with fused_softmax and without records")
+        if self.fused and not fused_softmax:
+            raise ValueError("the fused runner plays with fused_softmax")
+        if self.fused and record and autoreset:
+            raise ValueError("a recording fused runner plays whole games (no autoreset)")
         # fused_bookkeeping: ply counting and autoreset in one engine kernel (rvz_env_autoreset)
         # instead of ~12 small torch kernels per ply; the games are the same either way
         self.fused_bookkeeping = bool(fused_bookkeeping)
@@ -92,10 +94,20 @@ class SelfPlayRunner:
     def _body(self, plies: int = 1):
         eng = self.eng
         if self.fused:
+            rec, hist = None, None
+            if self.record:   # plies [ply_index, ply_index + plies) of the records, in place
+                k, n = self.ply_index, plies
+                if k + n > self.rec_idx.shape[0]:
+                    raise ValueError("records are full (max_plies)")
+                rec = (self.rec_black[k:k + n], self.rec_white[k:k + n], self.rec_side[k:k + n],
+                       self.rec_p[k:k + n])
+                hist = self.rec_idx[k:k + n]
             eng.play(self.evaluator, plies, self.temperature, self.seeds, self.seed_stride,
                      self._plies, self._done, reset=self.autoreset,
-                     skip_last_eval=self.skip_last_eval,
-                     games_per_workgroup=self.play_group)
+                     skip_last_eval=self.skip_last_eval, hist=hist,
+                     games_per_workgroup=self.play_group, records=rec)
+            if self.record:
+                self.post_status.copy_(eng.get_state()[2])
             return
         if self.record:          # the states before the move, for the game records
             b, w, st = eng.get_state()
@@ -128,8 +140,11 @@ class SelfPlayRunner:
     def capture(self, plies: int = 1):
         """Capture `plies` plies into one HIP graph (call after at least one eager ply warmed the
         kernels); ply() then replays them all (plies_per_call)."""
-        if plies < 1 or (plies > 1 and self.record):
-            raise ValueError("plies >= 1; a recording runner captures one ply per graph")
+        if plies < 1 or (plies > 1 and self.record and not self.fused) or (self.record and
+                                                                          self.fused):
+            raise ValueError("plies >= 1; a recording runner captures one ply per graph (the "
+                             "fused recording runner writes to the ply's record slice: use "
+                             "play_record)")
         torch.cuda.synchronize(self.eng.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -144,12 +159,23 @@ class SelfPlayRunner:
 
     plies_per_call = 1        # plies one ply() call plays (a captured multi-ply graph: more)
 
+    def play_record(self, plies: int):
+        """Fused recording runner: `plies` plies of every game in one rvz_play launch, recorded
+        into plies [ply_index, ply_index + plies) of the records."""
+        if not (self.fused and self.record):
+            raise ValueError("play_record is the fused recording runner's")
+        self._body(plies)
+        self.ply_index += plies
+
     def ply(self):
         """One ply of every game (a captured graph: plies_per_call plies)."""
         if self.graph is not None:
             self.graph.replay()
         else:
             self._body()
+        if self.record and self.fused:
+            self.ply_index += 1
+            return
         if self.record:
             k = self.ply_index
             self.rec_black[k].copy_(self.pre_black)

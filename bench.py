@@ -56,7 +56,7 @@ PRESETS = {   # BASELINE.json configs
                play_group=-16),
     # per GPU, x8; a step = one self-play + training iteration (main_c4)
     "c4": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, steps=1,
-               warmup=0, fused=False),
+               warmup=0, fused=True, play_group=-16),
     "c5": dict(games=16384, sims=400, blocks=6, filters=64, board=6, lanes=2, fused=True,
                play_group=-24),
 }
@@ -872,13 +872,20 @@ def main_c4(args, rank, world, device):
     spt = SelfPlayTrainer(net, args.games, args.sims, args.batch, 1.0, 1.0, seed=args.seed,
                           train_steps=args.train_steps, train_batch=args.train_batch,
                           graph=not args.no_graph, compact_leaves=not args.no_compact,
-                          memo=not args.no_memo)
-    # warm-up (untimed): one eager ply, the ply graph captured, two DDP steps on stand-in data
+                          memo=not args.no_memo, fused=args.fused,
+                          table_slots=args.table_slots if args.table else 0,
+                          table_discs=args.table_discs)
+    spt.runner.play_group = args.play_group
+    # warm-up (untimed): two plies (fused: one launch; else one eager ply and the ply graph
+    # captured), two DDP steps on stand-in data
     run = spt.runner
     run.start()
-    run.ply()
-    if not args.no_graph:
-        run.capture()
+    if args.fused:
+        run.play_record(2)
+    else:
+        run.ply()
+        if not args.no_graph:
+            run.capture()
     g = torch.Generator(device=device).manual_seed(rank)
     warm = {"states": (torch.rand(4 * args.train_batch, 3, args.board, args.board, device=device,
                                   generator=g) > 0.6).float(),
@@ -892,14 +899,13 @@ def main_c4(args, rank, world, device):
         spt.run_iteration()
     rdist.barrier()
     torch.cuda.synchronize(device)
+    rows0 = int(spt.eng.play_rows.item()) if args.fused else 0
+    hits0 = int(spt.eng.table_stats[0].item()) if args.fused else 0
     t0 = time.perf_counter()
     its = [spt.run_iteration() for _ in range(args.steps)]
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
-    if os.environ.get("RVZ_BENCH_ENQ"):
-        iv = np.diff(np.array([t0] + t_enq)) * 1e3
-        print(f"[bench] {args.config}: host enqueue ms per ply: {np.round(iv, 3).tolist()}; "
-              f"device total {(t1 - t0) * 1e3:.1f} ms", file=sys.stderr)
+    rows_sp = (int(spt.eng.play_rows.item()) - rows0) if args.fused else 0
     rdist.barrier()
     steps = sum(r["board_steps"] for r in its)
     total, dt, value = rdist.aggregate_rate(steps, t1 - t0)
@@ -919,21 +925,28 @@ def main_c4(args, rank, world, device):
     b.record()
     torch.cuda.synchronize(device)
     ar_ms = rdist.reduce_max(a.elapsed_time(b) / 20)
-    # the dominant kernel (the trunk) in isolation: HIP events over 10 back-to-back launches
     ev, eng = spt.evaluator, spt.eng
-    t_tr = isolated_trunk_ms(ev, eng.leaf_x)
-    fl = ev.mfma_flops_per_row() * eng.n_games
-    ach = fl / (t_tr * 1e-3) / 1e12
-    uach = ev.useful_flops_per_row() * eng.n_games / (t_tr * 1e-3) / 1e12
-    roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma", "achieved": round(ach, 2),
-            "peak": MFMA16_PEAK_TFLOPS, "unit": "TFLOP/s",
+    if args.fused:
+        # the dominant kernel is the iteration's one k_play launch (self-play of every game);
+        # its duration is the self-play phase's device-synchronised wall time
+        t_tr = sp_s / max(1, args.steps) * 1e3
+        rows_l = rows_sp / max(1, args.steps)
+        timing = ("the iteration's k_play launch: rows it evaluated (its own counter) over the "
+                  "self-play phase's device-synchronised wall time")
+    else:   # the trunk in isolation: HIP events over 10 back-to-back launches
+        t_tr = isolated_trunk_ms(ev, eng.leaf_x)
+        rows_l = eng.n_games
+        timing = "HIP events over 10 back-to-back full-batch launches after the timed region"
+    ach = ev.mfma_flops_per_row() * rows_l / (t_tr * 1e-3) / 1e12
+    uach = ev.useful_flops_per_row() * rows_l / (t_tr * 1e-3) / 1e12
+    roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma",
+            "achieved": round(ach, 2), "peak": MFMA16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / MFMA16_PEAK_TFLOPS, 4),
             "mfma_flops_per_row": ev.mfma_flops_per_row(),
             "useful_flops_per_row": ev.useful_flops_per_row(),
             "useful_frac": round(uach / MFMA16_PEAK_TFLOPS, 4), "traffic": None,
-            "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": eng.n_games,
-            "timing": "HIP events over 10 back-to-back full-batch launches after the timed "
-                      "region"}
+            "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": round(rows_l, 1),
+            "timing": timing}
     spt.eng.check()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -962,6 +975,13 @@ def main_c4(args, rank, world, device):
                        "parallelism": f"games sharded x{world}; DDP x{world} "
                                       f"({tdist.get_backend()})"},
             "selfplay_board_steps_per_s": round(sp_rate, 2),
+            "selfplay": ("fused: one rvz_play launch per iteration with device records, memo, "
+                         "deferred last batch and the cross-game table (a new generation per "
+                         "weight refresh)" if args.fused else "pull-style ply graph"),
+            "table": ({"hits_per_ply": round((int(spt.eng.table_stats[0].item()) - hits0) /
+                                            max(1, steps), 3),
+                       "nn_rows_per_ply": round(rows_sp / max(1, steps), 3)}
+                      if args.fused and args.table else None),
             "selfplay_s": round(sp_s, 3), "train_s": round(tr_s, 3),
             "ms_per_train_step": round(tr_s / max(1, n_train) * 1e3, 3),
             "allreduce": {"backend": tdist.get_backend(), "world": world,

@@ -205,6 +205,14 @@ typedef struct rvz_play_args {
                                     (every game commits `plies`). bench.py staggers the games'
                                     phases with it (game g at ply g mod 60 of its game) */
     int64_t *table_stats;        /* int64 [2] += {table hits, table inserts} (rvz_play_table), nullable */
+    /* Self-play records (self_play.py:88-101, the trainer's input; all four or none): for every
+     * act of the call, at [p][g] with p = the act's ply within the call, the position before the
+     * move (board bitboards and the side to move) and get_action_probs' vector (rec_p float64
+     * [plies][n_games][S*S+1]); hist holds the move. out_p is then not written. */
+    uint64_t *rec_black;         /* uint64 [plies][n_games], nullable */
+    uint64_t *rec_white;
+    int32_t *rec_side;           /* int32 [plies][n_games] */
+    double *rec_p;
 } rvz_play_args;
 /* A task-queue wait that times out (a workgroup waiting for its group's previous ply, bounded
  * spin) sets device error bit 16 (rvz_check): the other workgroups then stop drawing tasks and the

@@ -208,3 +208,41 @@ def test_c4_per_rank_shard_over_rccl_world1(oracle):
     for row, side, j in sides:
         want = 0.0 if win[j] == 0 else (1.0 if side == win[j] else -1.0)
         assert val[row] == want, (row, side, win[j])
+
+
+@pytest.mark.parametrize("table", [False, True])
+def test_fused_records_equal_the_pull_style_records(table):
+    """The fused recording runner (one rvz_play launch with device records: the position before
+    every act, its policy vector, the move) records exactly what the pull-style recording runner
+    copies out ply by ply (self_play.py:88-101), and the trainer arrays built from them are
+    equal (pipeline.py:179-246)."""
+    import rvz
+    from rvz.trainer import records_to_training
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 2, 64).cuda().eval()
+    G, S, P = 160, 128, 60
+    runs = []
+    for fused in (False, True):
+        eng = rvz.Engine(G, S, 64, compact_leaves=True, memo=True)
+        if fused and table:
+            eng.table(1 << 14, 14)
+        run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), record=True, max_plies=P,
+                                 seed_base=5, fused=fused, skip_last_eval=fused)
+        run.start()
+        if fused:
+            run.play_record(20)
+            run.play_record(P - 20)              # two launches: records land in their slices
+        else:
+            for _ in range(P):
+                run.ply()
+        run.check()
+        assert bool(run.post_status[:, 1].all())
+        runs.append(run)
+    a, b = runs
+    for name in ("rec_black", "rec_white", "rec_side", "rec_idx", "rec_p", "post_status"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    ta = records_to_training(a.rec_black, a.rec_white, a.rec_side, a.rec_idx, a.rec_p,
+                             a.post_status)
+    tb = records_to_training(b.rec_black, b.rec_white, b.rec_side, b.rec_idx, b.rec_p,
+                             b.post_status)
+    assert all(torch.equal(ta[k], tb[k]) for k in ta)
