@@ -73,6 +73,15 @@ __host__ __device__ constexpr int play_gpw_max() {
 // game flags: a row queued for the NN, its output ready for the expand, the game's plies done,
 // its row in this cycle's passes, its row held back last cycle (an odd row waits one cycle)
 enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4, PF_EVAL = 8, PF_HELD = 16 };
+// RVZ_PLAY_BALANCE 1: a search phase deals the games that take a turn (neither queued nor done)
+// round-robin over the waves from a list built before it, instead of game j to wave j % 4: a
+// group of 6 gives waves 0 and 1 two games each only when more than 4 games take a turn.
+// Measured neutral (C2 1.1022M vs 1.1022M, C5 4.196M vs 4.194M, 3 + 2 alternating pairs,
+// profiles/r04k_ab_balance.txt): the partner workgroup's tower fills the SIMD while a search
+// phase runs, so a shorter one buys nothing. Off (the validated order).
+#ifndef RVZ_PLAY_BALANCE
+#define RVZ_PLAY_BALANCE 0
+#endif
 constexpr int32_t ERR_SCHED = 16;   // a queue wait timed out (device error word)
 
 // ---- the cross-game NN-output table (rvz_play_table) ---------------------------------------
@@ -288,6 +297,8 @@ void k_play(PlayCtx ctx0) {
     __shared__ uint64_t q_bits[(GMAX + NBOARD) * 3];    // the same, in this cycle's row order
     __shared__ __attribute__((aligned(16))) float hin[HLDS ? GMAX * HROW : 4];   // heads rows
     __shared__ int q_rows[GMAX + 16];
+    __shared__ int s_act[GMAX];   // the games taking a turn in the next search phase
+    __shared__ int s_nact;
     __shared__ int s_nq;
     __shared__ float vpart[4][16];
     __shared__ int s_task[2];
@@ -380,13 +391,21 @@ void k_play(PlayCtx ctx0) {
                 st_f[j] = (bud && ply0 >= bud[g0 + j]) ? PF_DONE : 0;
                 st_p[j] = 0;
             }
+            if (RVZ_PLAY_BALANCE && tid == 0) {
+                int n = 0;
+                for (int j = 0; j < ng; ++j)
+                    if (!(bud && ply0 >= bud[g0 + j])) s_act[n++] = j;
+                s_nact = n;
+            }
         }
         __syncthreads();
         for (;;) {
             PT_NOW(t_c0);
             // search phase: each game not waiting for its row advances until it queues the next
             // row or has committed its plies (wave-uniform control flow per game)
-            for (int j = wave; j < ng; j += WPB) {
+            const int n_turn = RVZ_PLAY_BALANCE ? __builtin_amdgcn_readfirstlane(s_nact) : ng;
+            for (int it = wave; it < n_turn; it += WPB) {
+                const int j = RVZ_PLAY_BALANCE ? __builtin_amdgcn_readfirstlane(s_act[it]) : it;
                 const PlayCtx& c = play_ctx();
                 const View& v = c.v;
                 const PlayArgs& a = c.a;
@@ -574,8 +593,20 @@ void k_play(PlayCtx ctx0) {
                         n_ins += tab_insert<BS>(a, s_tgen, P, O, Vb, opaque_tid() & 63, q_rows[i]);
                 }
             }
-            for (int j = tid; j < ng; j += 256)
-                if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
+            if (RVZ_PLAY_BALANCE) {   // flags, and the list of the next search phase's games
+                if (tid == 0) {
+                    int n = 0;
+                    for (int j = 0; j < ng; ++j) {
+                        int fj = st_f[j];
+                        if (fj & PF_EVAL) st_f[j] = fj = (fj & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
+                        if (!(fj & (PF_QUEUED | PF_DONE))) s_act[n++] = j;
+                    }
+                    s_nact = n;
+                }
+            } else {
+                for (int j = tid; j < ng; j += 256)
+                    if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
+            }
             __syncthreads();
             PT_NOW(t_c4);
             PT_ADD(2, t_c4 - t_c3);
