@@ -73,14 +73,37 @@ def fixture_planes(path, n=None):
 def test_seeded_6x64_net_reproduces_reference_fixture():
     """torch.manual_seed(0) + rvz.AlphaZeroNetwork(8, 6, 64) is the reference's 6x64 net of the
     S=800 fixture (same module order and init): on CPU it reproduces the reference's recorded
-    softmax rows and values bit for bit, which pins the GPU evaluators against the reference's
-    own outputs (tests/test_gpu_network.py)."""
+    softmax rows bit for bit and its values within fp32 summation-order noise, which pins the
+    GPU evaluators against the reference's own outputs (tests/test_gpu_network.py).
+
+    The CPU's own summation order is host-dependent: on the fixture's recording host both were
+    bitwise; on an AVX512 EPYC host (round 4) the policy rows stay bitwise at one thread while
+    8.6% of the values differ by <= 5.6e-6 (values near 1 after tanh; both ours and the
+    fixture's are 1.4e-5 from the fp64 forward, so neither is the more accurate one). The
+    bound 1e-5 is the fp32-class tolerance the GPU evaluators are held to."""
     import rvz
     x, probs, value = fixture_planes(os.path.join(os.path.dirname(__file__), "golden",
                                                   "mcts_s800_6x64.npz"), n=256)
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 6, 64).eval()
-    with torch.no_grad():
-        logits, v = net(torch.from_numpy(x))
+    # one intra-op thread: the CPU conv's summation order depends on how the batch is split
+    # over threads (an 8-thread AVX512 host differs from the fixture in the last ulp of 0.9% of
+    # the entries; one thread reproduces it bit for bit)
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        with torch.no_grad():
+            logits, v = net(torch.from_numpy(x))
+    finally:
+        torch.set_num_threads(threads)
     assert np.array_equal(torch.softmax(logits, 1).numpy(), probs)
-    assert np.array_equal(v.numpy().reshape(-1), value)
+    v = v.numpy().reshape(-1)
+    assert np.abs(v - value).max() <= 1e-5, np.abs(v - value).max()
+    # the 64-bit reference forward of the same net is equally far from both (fp32 noise, not
+    # a different net): a wrong init would be orders of magnitude off
+    net64 = rvz.AlphaZeroNetwork(8, 6, 64).eval()
+    net64.load_state_dict(net.state_dict())
+    net64 = net64.double()
+    with torch.no_grad():
+        v64 = net64(torch.from_numpy(x).double())[1].numpy().reshape(-1)
+    assert np.abs(value - v64).max() <= 5e-5 and np.abs(v - v64).max() <= 5e-5
