@@ -11,9 +11,12 @@ batches, no NN rows), and applies its moves — the reference's ``current_player
 Results are then folded into the ratings in exactly the reference's game order, so the ELO
 history is what the sequential tournament would record for the same game outcomes.
 
-Randomness: each ply draws one ``random_sample()`` per game from a seeded NumPy generator and hands
-it to the mover's act kernel (the reference draws from the global NumPy RNG, game after game);
-random players (model None) pick with ``random.Random`` like ``random.choice`` (arena.py:178-180).
+Randomness (round 4): by default every game draws exactly what the reference's sequential
+tournament draws — one ``random_sample()`` per MCTS move from the NumPy stream and one
+``random.choice()`` per random-player move from the Python stream, game after game
+(arena.py:175-188, mcts.py:684) — so the same seeds give the reference's tournament; lockstep
+passes find each game's place in the streams (``Arena._play_reference_order``).
+``draw_order="batched"`` keeps round 3's cheaper order (one draw per game per ply).
 """
 from __future__ import annotations
 
@@ -118,34 +121,178 @@ class ELOPlayer:
         """Searches start from a fresh root every move (mcts.py:334): nothing to reset."""
 
 
+class _BatchedDraws:
+    """draw_order "batched": one random_sample() per game per ply from the arena's NumPy
+    generator (used by the games whose mover searches), random choices in (sorted player id,
+    game) order from its Python generator."""
+
+    def __init__(self, arena: "Arena"):
+        self.arena = arena
+        self.u = None
+
+    def begin_ply(self, G: int):
+        self.u = self.arena.np_rng.random_sample(G)
+
+    def uniforms(self, games: np.ndarray) -> np.ndarray:
+        u = np.zeros(len(self.u))
+        u[games] = self.u[games]
+        return u
+
+    def choice(self, g: int, sq: List[int]) -> int:
+        return self.arena.py_rng.choice(sq) if sq else -1
+
+
+class _ReferenceDraws:
+    """draw_order "reference", one pass: game g's MCTS moves take stream[offsets[g]],
+    stream[offsets[g] + 1], ...; its random moves use a Python generator started at states[g].
+    Counts what each game drew."""
+
+    def __init__(self, stream: np.ndarray, offsets: np.ndarray, states: List):
+        G = len(offsets)
+        self.stream = stream
+        self.ptr = [int(o) for o in offsets]
+        self.n_mcts = [0] * G
+        self.calls: List[List[int]] = [[] for _ in range(G)]
+        self.rng = []
+        for st in states:
+            r = random.Random()
+            r.setstate(st)
+            self.rng.append(r)
+
+    def begin_ply(self, G: int):
+        pass
+
+    def uniforms(self, games: np.ndarray) -> np.ndarray:
+        u = np.zeros(len(self.ptr))
+        for g in games:
+            if self.ptr[g] >= len(self.stream):
+                raise RuntimeError("Arena: draw stream exhausted (more MCTS moves than plies)")
+            u[g] = self.stream[self.ptr[g]]
+            self.ptr[g] += 1
+            self.n_mcts[g] += 1
+        return u
+
+    def choice(self, g: int, sq: List[int]) -> int:
+        if not sq:                      # arena.py:180: (-1, -1) without a draw
+            return -1
+        self.calls[g].append(len(sq))
+        return self.rng[g].choice(sq)
+
+
 class Arena:
-    def __init__(self, elo_system: Optional[ELORatingSystem] = None, seed: int = 0):
+    def __init__(self, elo_system: Optional[ELORatingSystem] = None, seed: int = 0,
+                 draw_order: str = "reference"):
+        """seed: the arena's NumPy and Python generators start as np.random.seed(seed) and
+        random.seed(seed) would leave the reference's global ones (the reference draws from
+        those, arena.py:178-188). draw_order: see ``play_games``."""
         self.elo = elo_system if elo_system is not None else ELORatingSystem()
         self.players: Dict[str, ELOPlayer] = {}
         self.np_rng = np.random.RandomState(seed)
         self.py_rng = random.Random(seed)
+        self.draw_order = draw_order
+        self.reference_order_passes = 0
 
     def add_player(self, player: ELOPlayer):
         self.players[player.player_id] = player
         self.elo.add_player(player.player_id)
 
     # ------------------------------------------------------------------ batched games
-    def play_games(self, black_ids: Sequence[str], white_ids: Sequence[str]) -> List[float]:
+    def play_games(self, black_ids: Sequence[str], white_ids: Sequence[str],
+                   draw_order: Optional[str] = None) -> List[float]:
         """Play len(black_ids) games in lockstep; game g has black_ids[g] (moves first) against
         white_ids[g]. Returns each game's result for its black player: 1.0 / 0.5 / 0.0
-        (arena.py:264-282). Every player that appears gets one engine over all games."""
+        (arena.py:264-282). Every player that appears gets one engine over all games.
+
+        draw_order (default: the arena's): "reference" draws exactly what the reference's
+        sequential loop draws (game after game from the global streams, arena.py:175-188,
+        mcts.py:684; see ``_play_reference_order``); "batched" draws one random_sample() per
+        game per ply and the random players' choices in (sorted player id, game) order."""
+        order = draw_order or self.draw_order
+        if order not in ("reference", "batched"):
+            raise ValueError(f"draw_order must be 'reference' or 'batched', got {order!r}")
         G = len(black_ids)
         if G == 0:
             return []
-        ids = sorted(set(black_ids) | set(white_ids))
-        for pid in ids:
+        for pid in set(black_ids) | set(white_ids):
             if pid not in self.players:
                 raise ValueError(f"One or both players not found: {pid}")
-        dev = next(iter(self.players[p].device for p in ids))
-        sizes = {self.players[p].board_size for p in ids if self.players[p].model is not None}
+        if order == "batched":
+            return self._lockstep(black_ids, white_ids, range(G), _BatchedDraws(self))
+        return self._play_reference_order(black_ids, white_ids)
+
+    def _play_reference_order(self, black_ids, white_ids) -> List[float]:
+        """The reference plays its games one after another, and every MCTS move draws one
+        random_sample() from NumPy's global stream (np.random.choice, mcts.py:684; none when all
+        visits are 0, mcts.py:679, which the engine refuses anyway), every random-player move one
+        random.choice() from Python's (arena.py:178-180). So game k's draws are a contiguous
+        piece of each stream, starting after everything games 0..k-1 drew.
+
+        Lockstep passes reproduce that exactly. A pass plays every game whose inputs changed
+        since the previous pass: its NumPy offset (the draws of the earlier games as the latest
+        pass counted them) and its Python generator state (the earlier games' choice() calls,
+        replayed in game order: a call's consumption depends only on len(seq)). A game's moves
+        are a function of those inputs alone (searches are per game, bit for bit), so a game
+        whose inputs did not change keeps its result. Game 0's inputs are exact from the start;
+        once games 0..k are exact, game k+1's inputs are, so the passes end (at most G + 1 of
+        them, two or three when only MCTS players meet: then the offsets depend only on the
+        earlier games' move counts). Both generators end where the sequential loop leaves them.
+        """
+        G = len(black_ids)
+        nsq = self._board_size(black_ids, white_ids) ** 2
+        mcts = {p: self.players[p].model is not None for p in set(black_ids) | set(white_ids)}
+        rs = np.random.RandomState()
+        rs.set_state(self.np_rng.get_state())
+        stream = rs.random_sample(G * (nsq - 4) + nsq)
+        py0 = self.py_rng.getstate()
+        # first guess: an MCTS player moves (nsq - 4) / 2 times per game
+        n_mcts = [(mcts[black_ids[g]] + mcts[white_ids[g]]) * (nsq - 4) // 2 for g in range(G)]
+        calls: List[List[int]] = [[] for _ in range(G)]
+        prev = [None] * G
+        results: List[Optional[float]] = [None] * G
+        self.reference_order_passes = 0
+        while True:
+            offsets = np.concatenate([[0], np.cumsum(n_mcts)[:-1]]).astype(np.int64)
+            r = random.Random()
+            r.setstate(py0)
+            states = []
+            for g in range(G):
+                states.append(r.getstate())
+                for n in calls[g]:
+                    r.choice(range(n))
+            inputs = [(int(offsets[g]), states[g]) for g in range(G)]
+            todo = [g for g in range(G) if inputs[g] != prev[g]]
+            if not todo:
+                break
+            draws = _ReferenceDraws(stream, offsets, states)
+            res = self._lockstep(black_ids, white_ids, todo, draws)
+            for g in todo:
+                results[g] = res[g]
+                n_mcts[g] = draws.n_mcts[g]
+                calls[g] = draws.calls[g]
+            prev = inputs
+            self.reference_order_passes += 1
+        total = int(sum(n_mcts))
+        if total:
+            self.np_rng.random_sample(total)
+        for g in range(G):
+            for n in calls[g]:
+                self.py_rng.choice(range(n))
+        return results
+
+    def _board_size(self, black_ids, white_ids) -> int:
+        sizes = {self.players[p].board_size for p in set(black_ids) | set(white_ids)
+                 if self.players[p].model is not None}
         if len(sizes) > 1:
             raise ValueError(f"players of one batch play on one board size, got {sorted(sizes)}")
-        bs = sizes.pop() if sizes else 8
+        return sizes.pop() if sizes else 8
+
+    def _lockstep(self, black_ids, white_ids, games, draws) -> List[Optional[float]]:
+        """Play `games` (indices into black_ids / white_ids) to their end in lockstep; the other
+        games start finished. draws supplies each MCTS move's uniform and each random move."""
+        G = len(black_ids)
+        ids = sorted(set(black_ids) | set(white_ids))
+        dev = next(iter(self.players[p].device for p in ids))
+        bs = self._board_size(black_ids, white_ids)
         nsq = bs * bs
         engines = {}
         for pid in ids:
@@ -155,6 +302,14 @@ class Arena:
                                       board_size=bs, device=dev, compact_leaves=True)
         env = Engine(G, 64, 64, board_size=bs, device=dev)   # the authoritative boards (env only)
         env.reset(range(G))
+        active = np.zeros(G, bool)
+        active[list(games)] = True
+        if not active.all():
+            b, w, st = env.get_state()
+            st = st.clone()
+            st[:, 1] = torch.where(torch.from_numpy(active).to(dev), st[:, 1],
+                                   torch.ones_like(st[:, 1]))
+            env.set_state(b.clone(), w.clone(), st)
         black = np.asarray([ids.index(b) for b in black_ids])
         white = np.asarray([ids.index(w) for w in white_ids])
         for _ in range(nsq - 4):                       # every move places a disc
@@ -164,7 +319,7 @@ class Arena:
                 break
             side = status[:, 0]
             mover = np.where(side == 1, black, white)  # index into ids per game
-            u = torch.from_numpy(self.np_rng.random_sample(G))
+            draws.begin_ply(G)
             move = np.full(G, -1, np.int64)
             for k, pid in enumerate(ids):
                 games_k = (mover == k) & (status[:, 1] == 0)
@@ -175,7 +330,7 @@ class Arena:
                     legal = env.legal().cpu().numpy().view(np.uint64)
                     for g in np.flatnonzero(games_k):
                         sq = [s for s in range(nsq) if (int(legal[g]) >> s) & 1]
-                        move[g] = self.py_rng.choice(sq) if sq else -1
+                        move[g] = draws.choice(g, sq)
                     continue
                 eng = engines[pid]
                 # this player's games only: the others enter its engine as finished (no search)
@@ -184,6 +339,7 @@ class Arena:
                                          torch.ones_like(st[:, 1]))
                 eng.set_state(b, w, st_k)
                 eng.search(pl.evaluator)
+                u = torch.from_numpy(draws.uniforms(np.flatnonzero(games_k)))
                 idx, _ = eng.act(1.0, u=u, apply=False)   # arena.py:183-186 uses T = 1.0
                 idx = idx.cpu().numpy()
                 move[games_k] = np.where(idx[games_k] == nsq, -1, idx[games_k])
@@ -197,10 +353,10 @@ class Arena:
             raise RuntimeError("Arena.play_games: a game is not over after its last ply")
         bb = b.cpu().numpy().view(np.uint64)
         ww = w.cpu().numpy().view(np.uint64)
-        res = []
-        for g in range(G):
+        res: List[Optional[float]] = [None] * G
+        for g in np.flatnonzero(active):
             nb, nw = bin(int(bb[g])).count("1"), bin(int(ww[g])).count("1")
-            res.append(1.0 if nb > nw else (0.0 if nw > nb else 0.5))
+            res[g] = 1.0 if nb > nw else (0.0 if nw > nb else 0.5)
         return res
 
     def play_game(self, player1_id: str, player2_id: str, verbose: bool = False,
@@ -237,8 +393,7 @@ class Arena:
         outcome = self.play_games([s[1] for s in schedule], [s[2] for s in schedule])
         for rnd in range(rounds):
             results["rounds"].append({"round": rnd + 1, "games": []})
-        for (rnd, p1, p2), r in zip(schedule, outcome):
-            e1b, e2b = self.elo.get_rating(p1), self.elo.get_rating(p2)
+        for n, ((rnd, p1, p2), r) in enumerate(zip(schedule, outcome)):
             self.elo.update_ratings(p1, p2, r)
             key = f"{p1}_vs_{p2}" if f"{p1}_vs_{p2}" in results["matchups"] else f"{p2}_vs_{p1}"
             m = results["matchups"][key]
@@ -251,11 +406,22 @@ class Arena:
                 m["wins2"] += 1
             else:
                 m["draws"] += 1
+            a1, a2 = self.elo.get_rating(p1), self.elo.get_rating(p2)
+            k, ex = self.elo.k, self.elo.get_expected_score
+            # arena.py:361-362 reconstructs the "before" ratings from the updated ones (with the
+            # expected score of the AFTER ratings), not the ratings the update started from;
+            # the reference's values are kept for drop-in results
             results["rounds"][rnd]["games"].append({
-                "player1": p1, "player2": p2, "result": r, "elo1_before": e1b,
-                "elo2_before": e2b, "elo1_after": self.elo.get_rating(p1),
-                "elo2_after": self.elo.get_rating(p2)})
-        if verbose or print_games:
+                "player1": p1, "player2": p2, "result": r,
+                "elo1_before": a1 - (k * (r - ex(a1, a2))),
+                "elo2_before": a2 - (k * ((1 - r) - ex(a2, a1))),
+                "elo1_after": a1, "elo2_after": a2})
+            if verbose or print_games:
+                if n + 1 == len(schedule) or schedule[n + 1][0] != rnd:
+                    print(f"\n--- After Round {rnd + 1} ---")
+                    self.print_leaderboard()
+        if not verbose and not print_games:
+            print("\n--- Tournament Complete ---")
             self.print_leaderboard()
         results["end_time"] = time.time()
         results["duration"] = results["end_time"] - results["start_time"]

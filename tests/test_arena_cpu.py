@@ -18,3 +18,63 @@ def test_elo_sequence_matches_reference(tmp_path):
     elo.save_ratings(str(path))
     again = ELORatingSystem.load_ratings(str(path))
     assert again.ratings == elo.ratings and again.games_played == elo.games_played
+
+
+def _fake_game(g, mcts_side, u_of, choice_of):
+    """A stand-in for one game's moves that consumes draws like an arena game: up to 12 moves,
+    sides alternate; an MCTS move takes one uniform and ends the game below 0.15, a random move
+    chooses among 1 + (7 t + g) mod 9 squares and ends the game on square 0. Returns a result
+    that depends on every draw."""
+    h = 0
+    for t in range(12):
+        if mcts_side[t % 2]:
+            u = u_of()
+            h = (h * 31 + int(u * 1e6)) % 1000003
+            if u < 0.15:
+                break
+        else:
+            m = choice_of(list(range(1 + (7 * t + g) % 9)))
+            h = (h * 31 + m) % 1000003
+            if m == 0:
+                break
+    return [0.0, 0.5, 1.0][h % 3]
+
+
+def test_reference_draw_order_passes_reproduce_sequential_draws(monkeypatch):
+    """Arena._play_reference_order's lockstep passes against the sequential loop, with the
+    game replaced by _fake_game (no GPU): same results and both generators end in the same
+    state, for MCTS-only, mixed and random-only schedules."""
+    import random
+    import types
+    import numpy as np
+    from rvz.arena import Arena
+
+    def fake_lockstep(self, black_ids, white_ids, games, draws):
+        G = len(black_ids)
+        draws.begin_ply(G)
+        res = [None] * G
+        for g in games:
+            side = (self.players[black_ids[g]].model is not None,
+                    self.players[white_ids[g]].model is not None)
+            res[g] = _fake_game(g, side, lambda: float(draws.uniforms(np.array([g]))[g]),
+                                lambda sq: draws.choice(g, sq))
+        return res
+
+    monkeypatch.setattr(Arena, "_lockstep", fake_lockstep)
+    for pairs in ([("a", "b")] * 5, [("a", "r"), ("r", "b"), ("a", "b"), ("r", "r")] * 4,
+                  [("r", "r")] * 6):
+        arena = Arena(seed=5)
+        for pid in "abr":
+            arena.players[pid] = types.SimpleNamespace(
+                model=None if pid == "r" else object(), board_size=8, device="cpu")
+        black = [p[0] for p in pairs]
+        white = [p[1] for p in pairs]
+        got = arena.play_games(black, white)
+        np_rng, py_rng = np.random.RandomState(5), random.Random(5)
+        want = [_fake_game(g, (b != "r", w != "r"), lambda: float(np_rng.random_sample()),
+                           py_rng.choice) for g, (b, w) in enumerate(pairs)]
+        assert got == want
+        assert arena.np_rng.random_sample() == np_rng.random_sample()
+        assert arena.py_rng.random() == py_rng.random()
+        assert arena.reference_order_passes <= len(pairs) + 1
+        print(pairs[:2], "passes", arena.reference_order_passes)
