@@ -217,6 +217,21 @@ __device__ __forceinline__ int h2_frag(int it, bool mirror) {
 #ifndef RVZ_H2_SKIP_LDS
 #define RVZ_H2_SKIP_LDS 0
 #endif
+// RVZ_H2_W128 1: the epilogue stores 16 bytes per lane (ds_write_b128, one per tile) after a
+// v_permlane16_swap exchange between lane quads, instead of two 8-byte stores (ds_write_b64),
+// which are 2-way bank-conflicted in any slot swizzle: a 16-lane ds_write_b64 group is 16 pixels
+// of one channel quad, which fill only 8 of the 16 8-byte bank positions modulo 32 banks. Eight
+// contiguous lanes of a b128 store are 8 consecutive pixel rows of one part, whose slots
+// (row mod 2, (row >> 1) & 3) cover the 32 banks once: conflict-free (tools/lds_banks.py).
+// C2's geometry only (ILV: F = 64, two 8x8 boards; the callers pass W128 = RVZ_H2_W128 && ILV):
+// at F = 128 and for three 6x6 boards the exchange's live registers push k_play from 256 / 255
+// VGPRs into spills. Measured and NOT kept (r04n, profiles/r04n_*): k_play's LDS bank conflicts
+// 10.7% -> 0.7% of LDS cycles, but C2 -0.8% on one box (3 alternating pairs, 1,042.4k vs
+// 1,034.1k; 233 -> 239 VGPRs, +2.8% VALU): a 2-way ds_write_b64 costs 8 LDS-array cycles against
+// its ~6 transfer cycles, while the swaps and the 13-cycle b128 transfer cost more.
+#ifndef RVZ_H2_W128
+#define RVZ_H2_W128 0
+#endif
 template <int CTW, int PTW>
 struct EpiH {
     f32x4 bias[CTW], isc[CTW];       // per out-channel bias, inverse weight scale
@@ -237,7 +252,7 @@ __device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __rest
 
 // v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
 // channels of one pixel per tile -> two 8-byte writes
-template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP>
+template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP, bool W128 = false>
 __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                                             const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
                                             const WaveTilesH<F, CTW, PTW>& wt, int lane,
@@ -278,8 +293,26 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                 d0[hf] = h0;
                 d1[hf] = h1;
             }
-            *reinterpret_cast<u32x2*>(out + o) = d0;
-            *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
+            if constexpr (W128) {
+                // lane quads 2k and 2k+1 (rows 2k, 2k+1 of 16 lanes) hold channels n8..n8+3 and
+                // n8+4..+7 of one pixel: v_permlane16_swap(d0, d1) moves the odd quad's part-0
+                // half into the even quad's d1 and the even quad's part-1 half into the odd
+                // quad's d0, so the even quad writes the 8 channels of part 0 and the odd quad
+                // those of part 1, 16 bytes each
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(d0[i], d1[i], false, false);
+                    d0[i] = r[0];
+                    d1[i] = r[1];
+                }
+                const int q = lane >> 4, n8 = (wt.ct0 + c) * H2_TM + 8 * (q >> 1);
+                const int o8 = C::at(wt.px[u], n8 / H2_K, (n8 % H2_K) >> 3) + (q & 1) * C::PLANE;
+                *reinterpret_cast<u32x4*>(out + o8) = u32x4{d0[0], d0[1], d1[0], d1[1]};
+            } else {
+                *reinterpret_cast<u32x2*>(out + o) = d0;
+                *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
+            }
         }
 }
 
@@ -418,8 +451,8 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 #endif
     }
     STEM_T(5);
-    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>::NPIX, CTW, PTW, false, true>(
-        out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>::NPIX, CTW, PTW, false, true,
+                RVZ_H2_W128 && ILV>(out, acc, er, wt, lane, ovf);
 }
 
 // The stem from the leaves' bitboards (the fused self-play kernel: select_phase leaves each
@@ -471,7 +504,7 @@ __device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
 #pragma unroll
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
     mma3<CTW, PTW, 0, 2>(acc, a, w);
-    epilogue_h2<F, G::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, G::NPIX, CTW, PTW, false, true, RVZ_H2_W128 && ILV>(out, acc, er, wt, lane, ovf);
 }
 
 template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0,
@@ -589,7 +622,8 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         }
         epilogue_heads<F, G::NPIX, CTW, PTW>(acc, er, wt, wave, lane, hw, hp.part, ovf);
     } else
-        epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
+        epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES, RVZ_H2_W128 && ILV>(out, acc, er, wt, lane,
+                                                                         ovf);
 }
 
 // the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for

@@ -10,7 +10,7 @@ of row r at q ^ ((r >> 1) & 3); off-board taps read zero row ZROW + (r & 7).
 B operand of v_mfma_f32_16x16x32_f16: lane l reads pixel tile*16 + (l & 15), slot l >> 4.
 Epilogue: lane l writes channels 4 (l >> 4) .. +3 of pixel tile*16 + (l & 15) (8 bytes).
 
-    python tools/lds_banks.py        # prints LDS cycles per read / write (ideal 4 / 4)
+    python tools/lds_banks.py        # LDS cycles per read / b64 write / b128 write (ideal 4 / 4 / 8)
 """
 READ_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
                list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
@@ -66,13 +66,36 @@ def write_cycles(nboard, swz):
     return tot / n
 
 
+def write128_cycles(nboard, swz):
+    """RVZ_H2_W128: after v_permlane16_swap, lane quad q writes 8 channels (16 B) of part q & 1,
+    channels 8 (q >> 1) .. +7 of its channel tile, at pixel tile*16 + (lane & 15); ds_write_b128
+    is serviced in 8 groups of 8 contiguous lanes, banks (a / 4) mod 32. The two parts are planes
+    PLANE halves apart (a multiple of 16 B; the part-1 plane is placed arbitrarily here: lanes of
+    one group never mix parts)."""
+    groups = [list(range(g, g + 8)) for g in range(0, 64, 8)]
+    plane = (nboard * 64 + 8) * 32 * 2                   # bytes of one part's k-step planes (KS=1)
+    tot, n = 0, 0
+    for pt in range(nboard * 4):
+        for ct in range(2):
+            addrs = {}
+            for lane in range(64):
+                q = lane >> 4
+                px = pt * 16 + (lane & 15)
+                n8 = ct * 16 + 8 * (q >> 1)
+                addrs[lane] = at(px, n8 >> 3, swz) + (q & 1) * plane
+            tot += group_cycles(addrs, groups, 16, 32)
+            n += 1
+    return tot / n
+
+
 def main():
     cur = lambda r: (r >> 1) & 3                        # noqa: E731
     first = lambda r: (r >> 1) & 2                      # noqa: E731  (the first h2 version)
     for name, swz, zr in (("(r>>1)&3, 8 zero rows", cur, 8), ("(r>>1)&2, 1 zero row", first, 1)):
         for nb, bs in ((2, 8), (2, 6), (1, 8), (1, 6)):
             print(f"{name:24s} NB={nb} {bs}x{bs}: read {read_cycles(nb, bs, swz, zr):.2f} "
-                  f"write {write_cycles(nb, swz):.2f} LDS cycles (ideal 4 / 4)")
+                  f"write b64 {write_cycles(nb, swz):.2f} (ideal 4) write b128 "
+                  f"{write128_cycles(nb, swz):.2f} (ideal 8) LDS cycles")
 
 
 if __name__ == "__main__":
