@@ -144,6 +144,11 @@ def parse(argv=None):
                          "together and stay in lockstep) instead of game g at ply g mod 60 of its "
                          "game (one budgeted rvz_play launch before the warm-up): without the "
                          "stagger a window shorter than a whole game measures one game phase")
+    ap.add_argument("--stagger-order", choices=("blocked", "interleaved"), default="blocked",
+                    help="which ply of its game the stagger puts global game g of N at (L = 60 "
+                         "on 8x8): blocked floor(g * L / N) (the games of a ply are consecutive, "
+                         "so a game group of the fused launch plays one ply of the game), "
+                         "interleaved g mod L; both put N / L games at every ply")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
@@ -320,21 +325,27 @@ def dispatch_summary():
     return out or None
 
 
-def stagger(args, runners, tag, device):
+def stagger(args, runners, tag, device, world=1):
     """Phase-neutral start: every game begins at the start position together,
     and 99.9% of 8x8 games last exactly 60 plies, so without this the games stay in lockstep and a
     window of fewer than 60 plies samples one game phase. One rvz_play launch with per-game ply
-    budgets puts global game g at ply g mod L of its first game (L = S*S - 4 = 60 on 8x8, the
-    length of a full game): from then on every ply of the run holds a whole game's mix of
-    phases, as continuous self-play does (self_play.py:80-101). Runs on each lane's engine (the
+    budgets puts global game g of N at ply floor(g * L / N) (--stagger-order blocked, the
+    default) or g mod L (interleaved) of its first game (L = S*S - 4 = 60 on 8x8, the length of
+    a full game): from then on every ply of the run holds a whole game's mix of phases, as
+    continuous self-play does (self_play.py:80-101), with N / L games at every ply either way.
+    Blocked keeps the games of one fused-launch group (consecutive games) at one ply, as
+    self-play's lockstep start does (one box: +0.6% over 60 plies, profiles/r04o_*). Runs on each lane's engine (the
     pull-style presets continue from the state k_play leaves:
     tests/test_gpu_play_oracle.py::test_stagger_then_pull_style_equals_fused). Returns the mean
     plies per game it played."""
     L = args.board * args.board - 4
+    n_global = args.games * world
     disp = Dispatches(play_kernel(args.board, args.filters), device, n=len(runners))
     tot, n = 0, 0
     for r in runners:
-        bud = ((r.seeds - args.seed) % L).to(torch.int32).contiguous()   # global game index mod L
+        gidx = r.seeds - args.seed                 # global game index
+        bud = (gidx * L // n_global if args.stagger_order == "blocked" else gidx % L)
+        bud = bud.to(torch.int32).contiguous()
         tot += int(bud.sum().item())
         n += bud.numel()
         disp(f"{tag}stagger", lambda r=r, bud=bud: r.eng.play(
@@ -630,7 +641,7 @@ def selfplay(args, device, rank, world, full=True):
     stagger_plies = 0.0
     if not args.no_stagger:
         stagger_plies = stagger(args, [lane0] if args.fused else
-                                (run.runners if args.lanes > 1 else [run]), tag, device)
+                                (run.runners if args.lanes > 1 else [run]), tag, device, world)
 
     # warmup: the first ply eager, then capture the ply graph with lane 0's trunk launches
     # stamping a ring of per-workgroup device wall-clock stamps, one row per launch (the heads
@@ -794,8 +805,11 @@ def selfplay(args, device, rank, world, full=True):
            "play_group": args.play_group if args.fused else None,
            "warmup_plies": {"stagger_mean": round(stagger_plies, 2),
                             "stagger": None if args.no_stagger else
-                            f"game g at ply g mod {args.board ** 2 - 4} of its game "
-                            "(one budgeted rvz_play launch)",
+                            f"game g of N at ply " + (
+                                f"floor(g * {args.board ** 2 - 4} / N)"
+                                if args.stagger_order == "blocked" else
+                                f"g mod {args.board ** 2 - 4}") +
+                            " of its game (one budgeted rvz_play launch)",
                             "after_stagger": warm_plies,
                             "total_mean": round(stagger_plies + warm_plies, 2)}}
     if full:

@@ -29,8 +29,11 @@ run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=
                          skip_last_eval=True, fused=True)
 run.play_group = int(os.environ.get("GROUP", -6))
 run.start()
-if int(os.environ.get("STAGGER", 1)):      # bench.py's phase stagger: game g at ply g mod 60
-    bud = ((run.seeds - 42) % 60).to(torch.int32).contiguous()
+if int(os.environ.get("STAGGER", 1)):      # bench.py's phase stagger (--stagger-order blocked:
+    # game g of G at ply floor(60 g / G); STAGGER=2: interleaved, g mod 60)
+    gi = run.seeds - 42
+    bud = (gi * 60 // G if int(os.environ.get("STAGGER", 1)) == 1 else gi % 60)
+    bud = bud.to(torch.int32).contiguous()
     eng.play(run.evaluator, 59, 1.0, run.seeds, run.seed_stride, run._plies, run._done,
              reset=True, skip_last_eval=True, games_per_workgroup=run.play_group, budget=bud)
 lib = rvz.load()
