@@ -123,8 +123,9 @@ int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, con
  * rvz_search_visits / rvz_act then back up the visit counts alone and return exactly the visits,
  * p and move of the evaluated search (tests/test_gpu_search.py::test_skip_last_eval_bit_exact).
  * Off unless called (one NN call fewer per move; not the reference's call sequence). bench.py's
- * headline uses it by default (--evals lazy: the memo + this, so the skipped evaluation is made
- * later only if a search reaches that position; rvz_play's skip_last_eval is the same). */
+ * headline uses it by default (--evals table, and --evals lazy: the memo + this, so the skipped
+ * evaluation is made later only if a search reaches that position; rvz_play's skip_last_eval is
+ * the same; --evals reference turns it off). */
 int rvz_search_skip(rvz_engine *e);
 /* Compacted leaf batches (on != 0; off by default): rvz_search_step writes the leaves that need an
  * evaluation (need[g] > 0; mcts.py:544-623 evaluates exactly those) to the first rows of their
