@@ -134,8 +134,9 @@ constexpr int WALK_STATS_MAX = 1 << 16;
 __device__ unsigned int g_walk[WALK_STATS_MAX][5];
 #define WALK_STAT(i, k) \
     if (lane == 0 && g < WALK_STATS_MAX) g_walk[g][i] += (k)
-// shader-clock split of a game's k_step work: [0] expand phase, [1] walk levels, [2] memory
-// backups of known terminals, [3] register fast path, [4] leaf (position, legal moves, queue)
+// shader-clock split of a game's k_step work: [0] expand phase (k_play: the cross-game table
+// lookups), [1] walk levels, [2] memory backups of known terminals, [3] register fast path,
+// [4] leaf (position, legal moves, queue)
 __device__ unsigned long long g_wtime[WALK_STATS_MAX][5];
 #define WT_NOW(t) const uint64_t t = __builtin_amdgcn_s_memtime()
 #define WT_ADD(i, t0) \

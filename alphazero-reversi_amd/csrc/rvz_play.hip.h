@@ -449,8 +449,11 @@ void k_play(PlayCtx ctx0) {
                             if (a.tab) {   // an earlier evaluation of this position: no new row
                                 const uint64_t P = st_bits[3 * j], O = st_bits[3 * j + 1],
                                                Vb = st_bits[3 * j + 2];
-                                if (__popcll(P | O) <= a.tmaxd &&
-                                    tab_lookup<BS>(a, s_tgen, P, O, Vb, lane, g)) {
+                                WT_NOW(ft_t);
+                                const bool hit = __popcll(P | O) <= a.tmaxd &&
+                                                 tab_lookup<BS>(a, s_tgen, P, O, Vb, lane, g);
+                                WT_ADD(0, ft_t);
+                                if (hit) {
                                     // the expand reads the row (and select's pend / path words)
                                     // back in this wave
                                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
