@@ -272,6 +272,11 @@ __device__ unsigned long long g_play_t[16384][12];
 #define PT_ADD(i, v)
 #endif
 
+// RVZ_PLAY_TOWER_PRIO (experiments): s_setprio for the evaluation phase (the trunk passes), 0
+// for the search and the FC heads
+#ifndef RVZ_PLAY_TOWER_PRIO
+#define RVZ_PLAY_TOWER_PRIO 0
+#endif
 template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_play(PlayCtx ctx0) {
@@ -554,6 +559,9 @@ void k_play(PlayCtx ctx0) {
             PT_NOW(t_c2);
 
             // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
+#if RVZ_PLAY_TOWER_PRIO
+            __builtin_amdgcn_s_setprio(RVZ_PLAY_TOWER_PRIO);   // experiments: tower over partner
+#endif
             for (int p0 = 0; p0 < nq; p0 += NBOARD) {
                 const PlayArgs& a = play_ctx().a;
                 int gb[NBOARD];
@@ -572,6 +580,9 @@ void k_play(PlayCtx ctx0) {
                         __builtin_amdgcn_readfirstlane(t >> 6), ovf);
                 __syncthreads();
             }
+#if RVZ_PLAY_TOWER_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             PT_NOW(t_c3);
             PT_ADD(1, t_c3 - t_c2);
             PT_ADD(5, (nq + NBOARD - 1) / NBOARD);
