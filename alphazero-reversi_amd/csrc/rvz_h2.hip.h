@@ -232,6 +232,14 @@ __device__ __forceinline__ int h2_frag(int it, bool mirror) {
 #ifndef RVZ_H2_W128
 #define RVZ_H2_W128 0
 #endif
+// RVZ_H2_PK 1: the epilogue's scale + bias fma and residual add on channel pairs (packed fp32
+// VALU), per element the same operations in the same order. Measured and NOT kept (r04u,
+// profiles/r04u_ab_pk.txt): the conv epilogue drops from ~144-194 to ~129-174 VALU instructions
+// per wave, k_play 233 -> 235 VGPRs, C2 -0.3% on one box (3 alternating pairs): the epilogue's
+// VALU already issues in the partner's MFMA shadow.
+#ifndef RVZ_H2_PK
+#define RVZ_H2_PK 0
+#endif
 template <int CTW, int PTW>
 struct EpiH {
     f32x4 bias[CTW], isc[CTW];       // per out-channel bias, inverse weight scale
@@ -275,6 +283,22 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 f32x2 v;
+                if constexpr (RVZ_H2_PK && !RVZ_H2_SKIP_LDS) {
+                    // the same per-element fma, add and max on channel pairs (v_pk_fma_f32,
+                    // v_pk_add_f32: one instruction per two values)
+                    const int j0 = 2 * hf;
+                    v = __builtin_elementwise_fma(f32x2{acc[c][u][j0], acc[c][u][j0 + 1]},
+                                                  f32x2{er.isc[c][j0], er.isc[c][j0 + 1]},
+                                                  f32x2{er.bias[c][j0], er.bias[c][j0 + 1]});
+                    if (RES) v = v + f32x2{er.res[c][u][j0], er.res[c][u][j0 + 1]};
+                    v = f32x2{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f)};
+                    ovf |= v[0] >= 65520.0f;
+                    ovf |= v[1] >= 65520.0f;
+                    if constexpr (KEEP) {
+                        er.res[c][u][j0] = v[0];
+                        er.res[c][u][j0 + 1] = v[1];
+                    }
+                } else
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int j = 2 * hf + e;
