@@ -272,6 +272,15 @@ __device__ unsigned long long g_play_t[16384][12];
 #define PT_ADD(i, v)
 #endif
 
+// RVZ_PLAY_SPLIT_LAST 1: the task queue's last ply is drawn as two tasks per group (its first
+// ceil(gpw / 2) games and the rest): a launch's end tail, where workgroups finish their last
+// tasks at spread-out times, is one half task instead of one task long. The games are the same
+// (a game's computation does not depend on which games share its task). Measured and NOT kept
+// (r04w, profiles/r04w_ab_split_last_*.txt): C2 -0.5% (20 plies) / -0.1% (60 plies) on one box:
+// a half task of 3 games runs fewer rows per pass and cycle than it saves in the tail.
+#ifndef RVZ_PLAY_SPLIT_LAST
+#define RVZ_PLAY_SPLIT_LAST 0
+#endif
 // RVZ_PLAY_TOWER_PRIO (experiments): s_setprio for the evaluation phase (the trunk passes), 0
 // for the search and the FC heads
 #ifndef RVZ_PLAY_TOWER_PRIO
@@ -306,7 +315,7 @@ void k_play(PlayCtx ctx0) {
     __shared__ int s_nact;
     __shared__ int s_nq;
     __shared__ float vpart[4][16];
-    __shared__ int s_task[2];
+    __shared__ int s_task[3];
     __shared__ unsigned s_tgen;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -317,7 +326,8 @@ void k_play(PlayCtx ctx0) {
         G = c.v.G;
         gpw = c.a.gpw;
         queue = c.a.q_next != nullptr;
-        total = queue ? c.a.n_groups * c.a.plies : 0;
+        // RVZ_PLAY_SPLIT_LAST: the last ply's tasks are half groups (2 n_groups tasks)
+        total = queue ? c.a.n_groups * (c.a.plies + (RVZ_PLAY_SPLIT_LAST ? 1 : 0)) : 0;
         task_plies = queue ? 1 : c.a.plies;
     }
     bool ovf = false;
@@ -332,7 +342,7 @@ void k_play(PlayCtx ctx0) {
     PT_NOW(t_start);
     for (int task_i = 0;; ++task_i) {
         // ---- the next task: a game group and the ply it starts at
-        int gi, ply0;
+        int gi, ply0, half = -1;
         if (!queue) {
             if (task_i > 0) break;
             gi = blockIdx.x;
@@ -350,10 +360,17 @@ void k_play(PlayCtx ctx0) {
                     failed ? (unsigned)total
                            : __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-                int tg = -1, tp = 0;
+                int tg = -1, tp = 0, th = -1;
                 if ((int)t < total) {
-                    tg = (int)(t % (unsigned)a.n_groups);
-                    tp = (int)(t / (unsigned)a.n_groups);
+                    const unsigned full = (unsigned)a.n_groups * (unsigned)(a.plies - 1);
+                    if (RVZ_PLAY_SPLIT_LAST && t >= full) {   // a half of group tg, last ply
+                        tg = (int)((t - full) >> 1);
+                        th = (int)((t - full) & 1u);
+                        tp = a.plies - 1;
+                    } else {
+                        tg = (int)(t % (unsigned)a.n_groups);
+                        tp = (int)(t / (unsigned)a.n_groups);
+                    }
                     // the group's previous ply: played (and published) by the workgroup that
                     // drew it n_groups tasks ago, which is running; bounded spin, abandoned as
                     // soon as another workgroup's wait timed out
@@ -377,18 +394,27 @@ void k_play(PlayCtx ctx0) {
                 }
                 s_task[0] = tg;
                 s_task[1] = tp;
+                s_task[2] = th;
             }
             __syncthreads();   // the other waves load the group's state after the acquire
             gi = __builtin_amdgcn_readfirstlane(s_task[0]);
             ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
+            half = __builtin_amdgcn_readfirstlane(s_task[2]);
             if (gi < 0) break;
             PT_NOW(t_q1);
             PT_ADD(8, t_q1 - t_q0);
             PT_ADD(9, 1);
         }
-        const int g0 = gi * gpw;
-        const int ng = min(gpw, G - g0);
-        if (ng <= 0) break;
+        // half >= 0: games [h0, h0 + hn) of the group only (the last ply's half tasks)
+        const int h0 = half <= 0 ? 0 : (gpw + 1) / 2;
+        const int hn = half < 0 ? gpw : (half == 0 ? (gpw + 1) / 2 : gpw / 2);
+        const int g0 = gi * gpw + h0;
+        const int ng = min(hn, G - g0);
+        if (ng <= 0) {   // an empty half task (gpw 1, or the last group's second half)
+            if (!queue) break;
+            __syncthreads();   // every wave has read s_task before wave 0 draws the next task
+            continue;
+        }
         {   // a game whose ply budget this task's ply reaches starts done
             const int32_t* bud = play_ctx().a.budget;
             for (int j = tid; j < ng; j += 256) {
