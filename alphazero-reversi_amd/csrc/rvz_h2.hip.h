@@ -240,10 +240,23 @@ __device__ __forceinline__ int h2_frag(int it, bool mirror) {
 #ifndef RVZ_H2_PK
 #define RVZ_H2_PK 0
 #endif
+// The trunk's register / prefetch knobs as a type (the fused kernels instantiate more than one):
+// SKIP = RVZ_H2_SKIP_LDS, APD / PD = the activation / weight prefetch distances in k-steps
+template <bool SKIP_, int APD_, int PD_>
+struct H2Knobs {
+    static constexpr bool SKIP = SKIP_;
+    static constexpr int APD = APD_, PD = PD_;
+    static_assert(PD_ >= 1 && PD_ <= 4 && APD_ >= 0, "prefetch distances");
+};
+using H2Def = H2Knobs<RVZ_H2_SKIP_LDS != 0, RVZ_H2_APD, RVZ_H2_PD>;
+// the trunk at <= 168 VGPRs (three waves per SIMD): skip input from LDS, no activation prefetch,
+// weights one k-step ahead (profiles/r04v_ab_trunk_register_diet.json: 166 VGPRs, 3.8% slower
+// alone)
+using H2Diet = H2Knobs<true, 0, 1>;
 template <int CTW, int PTW>
 struct EpiH {
     f32x4 bias[CTW], isc[CTW];       // per out-channel bias, inverse weight scale
-    float res[CTW][PTW][RVZ_H2_SKIP_LDS ? 1 : 4];   // the block input (fp32) of this lane's outputs
+    float res[CTW][PTW][4];          // the block input (fp32) of this lane's outputs (SKIP: unused)
 };
 
 template <int F, int CTW, int PTW>
@@ -260,7 +273,8 @@ __device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __rest
 
 // v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
 // channels of one pixel per tile -> two 8-byte writes
-template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP, bool W128 = false>
+template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP, bool W128 = false,
+          bool SKIP = RVZ_H2_SKIP_LDS != 0>
 __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                                             const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
                                             const WaveTilesH<F, CTW, PTW>& wt, int lane,
@@ -275,7 +289,7 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
             const int n0 = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
             const int o = C::at(wt.px[u], n0 / H2_K, (n0 % H2_K) >> 3) + (n0 & 4);
             f16x4 s0, s1;
-            if (RES && RVZ_H2_SKIP_LDS) {
+            if (RES && SKIP) {
                 s0 = *reinterpret_cast<const f16x4*>(out + o);
                 s1 = *reinterpret_cast<const f16x4*>(out + C::PLANE + o);
             }
@@ -283,7 +297,7 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 f32x2 v;
-                if constexpr (RVZ_H2_PK && !RVZ_H2_SKIP_LDS) {
+                if constexpr (RVZ_H2_PK && !SKIP) {
                     // the same per-element fma, add and max on channel pairs (v_pk_fma_f32,
                     // v_pk_add_f32: one instruction per two values)
                     const int j0 = 2 * hf;
@@ -304,12 +318,12 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                     const int j = 2 * hf + e;
                     float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]);
                     if (RES) {
-                        if constexpr (RVZ_H2_SKIP_LDS) x += (float)s0[j] + (float)s1[j];
+                        if constexpr (SKIP) x += (float)s0[j] + (float)s1[j];
                         else x += er.res[c][u][j];
                     }
                     x = fmaxf(x, 0.0f);
                     ovf |= x >= 65520.0f;
-                    if constexpr (KEEP && !RVZ_H2_SKIP_LDS) er.res[c][u][j] = x;
+                    if constexpr (KEEP && !SKIP) er.res[c][u][j] = x;
                     v[e] = x;
                 }
                 uint32_t h0, h1;
@@ -532,16 +546,16 @@ __device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
 }
 
 template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0,
-          bool LASTH = false>
+          bool LASTH = false, class K = H2Def>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                         const H2W& wr, int wl,   // layer base, f16x8 units
                                         const float* __restrict__ bias,
                                         const float* __restrict__ isc, int wave, int lane,
-                                        f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
+                                        f16x8 (&bc)[K::PD][CTW][2], EpiH<CTW, PTW>& er,
                                         bool& ovf, HeadPart hp = HeadPart{}) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     using C = CfgH<F, G::NPIX>;
-    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
+    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = K::PD, APD = K::APD;
     // ILV: tile 0 is board row 0 (pixel group 0) or row 7 (group 1), and the taps with dr = -1
     // (row 0) or dr = +1 (row 7) leave the boards for all its pixels: tile 0's A loads and MFMAs
     // are skipped in those k-steps (1/12 of the conv MFMAs).
@@ -646,8 +660,8 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         }
         epilogue_heads<F, G::NPIX, CTW, PTW>(acc, er, wt, wave, lane, hw, hp.part, ovf);
     } else
-        epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES, RVZ_H2_W128 && ILV>(out, acc, er, wt, lane,
-                                                                         ovf);
+        epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES, RVZ_H2_W128 && ILV, K::SKIP>(out, acc, er,
+                                                                                  wt, lane, ovf);
 }
 
 // the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for
@@ -720,12 +734,14 @@ struct HeadsInLds {
 // bits is set, the bitboards bits[3 * b .. 3 * b + 2] = (P, O, V) (LDS). Output: the 1x1
 // head-conv rows through hout (HeadsGlobalIdx: row gb[b] of work; HeadsInLds: the FC heads' LDS
 // input rows).
-template <int F, int NBOARD, int CTW, int PTW, int BS, class HOut>
+template <int F, int NBOARD, int CTW, int PTW, int BS, class HOut, class K = H2Def,
+          class Bar = BarWG>
 __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
                                         const int (&gbv)[NBOARD], const uint64_t* bits,
                                         const float* __restrict__ prm, const Layout& L,
                                         const uint16_t* __restrict__ blob, int n_blocks,
-                                        const HOut& hout, int tid, int lane, int wave, bool& ovf) {
+                                        const HOut& hout, int tid, int lane, int wave, bool& ovf,
+                                        const Bar& bar = Bar{}) {
     using WT = WaveTilesH<F, CTW, PTW>;
     constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
@@ -750,15 +766,15 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     // from the weight prefetch to the last residual block; NAT (RVZ_H2_MIRROR 0): one instance
     // per pixel group (its own tile-0 skip window), chosen by a wave-uniform branch
     const bool grp1 = ILV && RVZ_H2_MIRROR == 0 && wave / WT::CG != 0;
-    constexpr bool HEPI = RVZ_H2_HEADS_EPI && !RVZ_H2_SKIP_LDS && ILV;   // C2 shape (F = 128 spilled)
+    constexpr bool HEPI = RVZ_H2_HEADS_EPI && !K::SKIP && ILV;   // C2 shape (F = 128 spilled)
     auto trunk = [&](auto grp) {
         constexpr int GR = decltype(grp)::value;
-        f16x8 bc[RVZ_H2_PD][CTW][2];
+        f16x8 bc[K::PD][CTW][2];
         if (n_blocks > 0) {
             const int wu = WT(wave, lane).ct0 * 64;
             const bool mirror = ILV && RVZ_H2_MIRROR != 0 && wave / WT::CG != 0;   // as conv_h2
 #pragma unroll
-            for (int s = 0; s < RVZ_H2_PD; ++s) {
+            for (int s = 0; s < K::PD; ++s) {
                 const int f = wu + h2_frag<F>(s, mirror);
 #pragma unroll
                 for (int c = 0; c < CTW; ++c)
@@ -787,12 +803,12 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
             STEM_T(0);
             st.store(xin, tid);
             STEM_T(1);
-            __syncthreads();
+            bar();
             STEM_T(2);
             stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
             STEM_T(3);
         }
-        __syncthreads();
+        bar();
         PHASE(1);
         {
             PASS_NOW(tp1);
@@ -802,28 +818,28 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
         const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
         for (int blk = 0; blk < n_blocks - (HEPI ? 1 : 0); ++blk) {
             const int l1 = 2 * blk, l2 = 2 * blk + 1;
-            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
+            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR, false, K>(actA, actB, wr, (int)(l1 * LW / 8),
                                                           prm + L.res_b + (size_t)l1 * F,
                                                           isc + l1 * F, wave, lane, bc, er, ovf);
             if (blk == 0) PHASE(5);
-            __syncthreads();
+            bar();
             if (blk == 0) PHASE(6);
-            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR>(actB, actA, wr, (int)(l2 * LW / 8),
+            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, false, K>(actB, actA, wr, (int)(l2 * LW / 8),
                                                          prm + L.res_b + (size_t)l2 * F,
                                                          isc + l2 * F, wave, lane, bc, er, ovf);
-            __syncthreads();
+            bar();
         }
         if (HEPI && n_blocks > 0) {   // the last block: its conv B ends in the head convs
             const int l1 = 2 * n_blocks - 2, l2 = 2 * n_blocks - 1;
-            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
+            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR, false, K>(actA, actB, wr, (int)(l1 * LW / 8),
                                                           prm + L.res_b + (size_t)l1 * F,
                                                           isc + l1 * F, wave, lane, bc, er, ovf);
-            __syncthreads();
-            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, true>(
+            bar();
+            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, true, K>(
                 actB, actA, wr, (int)(l2 * LW / 8), prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
                 wave, lane, bc, er, ovf,
                 HeadPart{prm + L.pol_w, prm + L.val_w, reinterpret_cast<float*>(actA)});
-            __syncthreads();
+            bar();
         }
     };
     if (grp1)
@@ -851,7 +867,7 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     } else {
         head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA},
                                                   reinterpret_cast<float*>(actB), prm, L, hout,
-                                                  tid);
+                                                  tid, bar);
     }
 #ifdef RVZ_PLAY_TIMING
     {

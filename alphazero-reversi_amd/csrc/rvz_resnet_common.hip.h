@@ -55,11 +55,16 @@ __host__ __device__ inline Layout make_layout(int F, int NB, int BS = 8) {
 // (cells = BS*BS), hpv(b)[0 .. 2 cells) = the policy planes (NCHW flatten, the FC's input order)
 // and hpv(b)[2 cells .. 3 cells) = the value plane. A BS < 8 board sits in the top-left corner
 // of the 8x8 pixel grid.
+// The barrier the evaluator device functions use between their phases: the workgroup's
+// (__syncthreads) by default; the fused kernel's teams pass their own (a 4-wave barrier in LDS)
+struct BarWG {
+    __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
 template <int F, int NBOARD, int NTHR, int BS = 8, bool PACKED = false, bool ILV = false, class Act,
-          class Out>
+          class Out, class Bar = BarWG>
 __device__ __forceinline__ void head_convs(const Act& act, float* part,
                                            const float* __restrict__ prm, const Layout& L,
-                                           const Out& hpv, int tid) {
+                                           const Out& hpv, int tid, const Bar& bar = Bar{}) {
     constexpr int NW = NTHR / 64, CG = NW / NBOARD, CPG = F / CG;
     static_assert(CPG % 8 == 0, "8-channel reads");
     const int lane = tid & 63;
@@ -91,7 +96,7 @@ __device__ __forceinline__ void head_convs(const Act& act, float* part,
         part[(cg * 3 + 1) * NBOARD * 64 + row] = p1;
         part[(cg * 3 + 2) * NBOARD * 64 + row] = p2;
     }
-    __syncthreads();
+    bar();
     constexpr int CELLS = BS * BS;
     for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
         const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
@@ -182,12 +187,12 @@ __host__ __device__ constexpr int heads_in_floats(int BS) {
 // INROWS < 16: `in` holds INROWS rows and column c reads row c % INROWS (columns past the
 // rows are not stored: their outputs are discarded)
 template <int BS, class Rows, bool STREAM = RVZ_HEADS_STREAM != 0, bool COPY = true,
-          int INROWS = 16>
+          int INROWS = 16, class Bar = BarWG>
 __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const Rows& rmap,
                                            const float* __restrict__ prm, const Layout& L,
                                            float* __restrict__ logits, float* __restrict__ value,
                                            float* __restrict__ in, float (*vpart)[16],
-                                           int tid = threadIdx.x) {
+                                           int tid = threadIdx.x, const Bar& bar = Bar{}) {
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
     constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
     constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
@@ -273,7 +278,7 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
             *reinterpret_cast<f32x4*>(in + b * ROW + k) = v[q];
         }
     }
-    __syncthreads();
+    bar();
 #ifdef RVZ_PLAY_TIMING
     if constexpr (!STREAM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
@@ -371,14 +376,14 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
         policy_tile(t, acc);
     }
     }
-    __syncthreads();
+    bar();
     if (tid < 16) {
         const int rt = rmap.row(tid);
         if (rt >= 0)
             value[rt] = tanhf(((vpart[0][tid] + vpart[1][tid]) + (vpart[2][tid] + vpart[3][tid])) +
                               prm[L.vfc2_b]);
     }
-    __syncthreads();
+    bar();
     PASS_NOW(th2);
     if constexpr (!STREAM) PASS_ADD(5, th2 - th1);
 }
