@@ -242,13 +242,18 @@ __device__ __forceinline__ int h2_frag(int it, bool mirror) {
 #endif
 // The trunk's register / prefetch knobs as a type (the fused kernels instantiate more than one):
 // SKIP = RVZ_H2_SKIP_LDS, APD / PD = the activation / weight prefetch distances in k-steps
-template <bool SKIP_, int APD_, int PD_>
+// LATE: the epilogue's bias and inverse scales are loaded after the k-loop instead of before it
+// (16 fewer VGPRs held through the loop; the load's latency is then exposed at each epilogue)
+template <bool SKIP_, int APD_, int PD_, bool LATE_ = false>
 struct H2Knobs {
-    static constexpr bool SKIP = SKIP_;
+    static constexpr bool SKIP = SKIP_, LATE = LATE_;
     static constexpr int APD = APD_, PD = PD_;
     static_assert(PD_ >= 1 && PD_ <= 4 && APD_ >= 0, "prefetch distances");
 };
-using H2Def = H2Knobs<RVZ_H2_SKIP_LDS != 0, RVZ_H2_APD, RVZ_H2_PD>;
+#ifndef RVZ_H2_LATE_EPI
+#define RVZ_H2_LATE_EPI 0
+#endif
+using H2Def = H2Knobs<RVZ_H2_SKIP_LDS != 0, RVZ_H2_APD, RVZ_H2_PD, RVZ_H2_LATE_EPI != 0>;
 // the trunk at <= 168 VGPRs (three waves per SIMD): skip input from LDS, no activation prefetch,
 // weights one k-step ahead (profiles/r04v_ab_trunk_register_diet.json: 166 VGPRs, 3.8% slower
 // alone)
@@ -579,7 +584,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         if (NAT) return GRP == 0 ? i < 3 * KS : (i >= 6 * KS && i < 9 * KS);
         return i < 3 * KS;
     };
-    load_epi(er, bias, isc, wt, lane);                // lands during the k-loop
+    if constexpr (!K::LATE) load_epi(er, bias, isc, wt, lane);   // lands during the k-loop
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
     unsigned pmask[PTW];                              // valid taps in iteration order
 #pragma unroll
@@ -648,6 +653,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
             for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
+    if constexpr (K::LATE) load_epi(er, bias, isc, wt, lane);
     // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
     if constexpr (LASTH) {
         f32x4 hw[3][CTW];                             // the head convs' weights (L2, once)

@@ -26,6 +26,15 @@
 #ifndef RVZ_T12_SLOTS
 #define RVZ_T12_SLOTS 2
 #endif
+// the trunk teams' knobs (<= 168 VGPRs): 0 H2Diet (no activation prefetch, weights 1 k-step
+// ahead); 1 activation prefetch 1, weights 1 ahead, epilogue operands loaded late; 2 no activation
+// prefetch, weights 2 ahead, epilogue operands late
+#ifndef RVZ_T12_KNOBS
+#define RVZ_T12_KNOBS 0
+#endif
+using T12K = std::conditional_t<RVZ_T12_KNOBS == 1, H2Knobs<true, 1, 1, true>,
+                                std::conditional_t<RVZ_T12_KNOBS == 2, H2Knobs<true, 0, 2, true>,
+                                                   H2Diet>>;
 constexpr int T12_TW = 4;                   // waves per team
 constexpr int T12_NSLOT = RVZ_T12_SLOTS;    // task slots of the search team
 constexpr int T12_SG = T12_NSLOT > 2 ? 6 : 8;   // games per slot at most (LDS: the heads rows)
@@ -207,7 +216,7 @@ void k_play12(PlayCtx ctx0) {
 #pragma unroll
                 for (int b = 0; b < NBOARD; ++b) gb[b] = -1;   // bitboard stem: no planes read
                 const int t = opaque_tid() & 255;
-                h2_pass<F, NBOARD, CTW, PTW, BS, HeadsSlots12<BS>, H2Diet, TeamBar>(
+                h2_pass<F, NBOARD, CTW, PTW, BS, HeadsSlots12<BS>, T12K, TeamBar>(
                     smem[team], a.x, gb, tbits[team], a.prm, a.L, a.blob, a.n_blocks, hout, t,
                     t & 63, __builtin_amdgcn_readfirstlane((t >> 6) & 3), ovf, tb);
             }
