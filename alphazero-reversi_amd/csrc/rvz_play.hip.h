@@ -399,7 +399,7 @@ void k_play(PlayCtx ctx0) {
             __syncthreads();   // the other waves load the group's state after the acquire
             gi = __builtin_amdgcn_readfirstlane(s_task[0]);
             ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
-            half = __builtin_amdgcn_readfirstlane(s_task[2]);
+            half = RVZ_PLAY_SPLIT_LAST ? __builtin_amdgcn_readfirstlane(s_task[2]) : -1;
             if (gi < 0) break;
             PT_NOW(t_q1);
             PT_ADD(8, t_q1 - t_q0);
@@ -410,7 +410,7 @@ void k_play(PlayCtx ctx0) {
         const int hn = half < 0 ? gpw : (half == 0 ? (gpw + 1) / 2 : gpw / 2);
         const int g0 = gi * gpw + h0;
         const int ng = min(hn, G - g0);
-        if (ng <= 0) {   // an empty half task (gpw 1, or the last group's second half)
+        if (RVZ_PLAY_SPLIT_LAST && ng <= 0) {   // an empty half task (gpw 1, or the last group's second half)
             if (!queue) break;
             __syncthreads();   // every wave has read s_task before wave 0 draws the next task
             continue;
