@@ -325,6 +325,13 @@ def dispatch_summary():
     return out or None
 
 
+def stagger_budget(gidx: torch.Tensor, L: int, n_global: int, order: str) -> torch.Tensor:
+    """The ply of its game each global game index starts the run at (the stagger launch's
+    per-game budgets): blocked floor(g * L / N), interleaved g mod L."""
+    bud = gidx * L // n_global if order == "blocked" else gidx % L
+    return bud.to(torch.int32).contiguous()
+
+
 def stagger(args, runners, tag, device, world=1):
     """Phase-neutral start: every game begins at the start position together,
     and 99.9% of 8x8 games last exactly 60 plies, so without this the games stay in lockstep and a
@@ -334,8 +341,9 @@ def stagger(args, runners, tag, device, world=1):
     a full game): from then on every ply of the run holds a whole game's mix of phases, as
     continuous self-play does (self_play.py:80-101), with N / L games at every ply either way.
     Blocked keeps the games of one fused-launch group (consecutive games) at one ply, as
-    self-play's lockstep start does (one box: +0.6% over 60 plies, profiles/r04o_*). Runs on each lane's engine (the
-    pull-style presets continue from the state k_play leaves:
+    self-play's lockstep start does (one box: +0.8% / +0.9% in 20- / 60-ply windows,
+    profiles/r04o_ab_stagger_order_*). Runs on each lane's engine (the pull-style presets
+    continue from the state k_play leaves:
     tests/test_gpu_play_oracle.py::test_stagger_then_pull_style_equals_fused). Returns the mean
     plies per game it played."""
     L = args.board * args.board - 4
@@ -343,9 +351,7 @@ def stagger(args, runners, tag, device, world=1):
     disp = Dispatches(play_kernel(args.board, args.filters), device, n=len(runners))
     tot, n = 0, 0
     for r in runners:
-        gidx = r.seeds - args.seed                 # global game index
-        bud = (gidx * L // n_global if args.stagger_order == "blocked" else gidx % L)
-        bud = bud.to(torch.int32).contiguous()
+        bud = stagger_budget(r.seeds - args.seed, L, n_global, args.stagger_order)
         tot += int(bud.sum().item())
         n += bud.numel()
         disp(f"{tag}stagger", lambda r=r, bud=bud: r.eng.play(

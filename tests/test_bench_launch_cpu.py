@@ -136,3 +136,25 @@ def test_spawn_ranks_terminates_children_when_the_launcher_is_killed(tmp_path):
     for pid in pids:
         with pytest.raises(ProcessLookupError):
             os.kill(pid, 0)
+
+
+@pytest.mark.parametrize("order", ["blocked", "interleaved"])
+@pytest.mark.parametrize("n,L,world", [(4096, 60, 1), (16384, 32, 1), (32768, 60, 8), (1000, 60, 2)])
+def test_stagger_budgets_are_phase_neutral(order, n, L, world):
+    """bench.py's stagger: every ply of the game holds N / L games (floor or
+    ceil), whichever order, and the per-rank shards of the global index space together give the
+    single-process budgets; blocked keeps every fused-launch group of 6 consecutive games within
+    two adjacent plies."""
+    import torch
+    import bench
+    G = n * world
+    full = bench.stagger_budget(torch.arange(G, dtype=torch.int64), L, G, order)
+    counts = torch.bincount(full.long(), minlength=L)
+    assert counts.numel() == L and int(counts.min()) >= G // L and int(counts.max()) <= -(-G // L)
+    assert int(full.min()) >= 0 and int(full.max()) <= L - 1
+    parts = [bench.stagger_budget(torch.arange(r * n, (r + 1) * n, dtype=torch.int64), L, G, order)
+             for r in range(world)]
+    assert torch.equal(torch.cat(parts), full)
+    if order == "blocked":
+        groups = full[: G // 6 * 6].view(-1, 6)
+        assert int((groups.max(1).values - groups.min(1).values).max()) <= 1
