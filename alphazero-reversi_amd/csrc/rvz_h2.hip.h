@@ -740,14 +740,17 @@ struct HeadsInLds {
 // bits is set, the bitboards bits[3 * b .. 3 * b + 2] = (P, O, V) (LDS). Output: the 1x1
 // head-conv rows through hout (HeadsGlobalIdx: row gb[b] of work; HeadsInLds: the FC heads' LDS
 // input rows).
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
 template <int F, int NBOARD, int CTW, int PTW, int BS, class HOut, class K = H2Def,
-          class Bar = BarWG>
+          class Bar = BarWG, class Hook = NoHook>
 __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
                                         const int (&gbv)[NBOARD], const uint64_t* bits,
                                         const float* __restrict__ prm, const Layout& L,
                                         const uint16_t* __restrict__ blob, int n_blocks,
                                         const HOut& hout, int tid, int lane, int wave, bool& ovf,
-                                        const Bar& bar = Bar{}) {
+                                        const Bar& bar = Bar{}, const Hook& hook = Hook{}) {
     using WT = WaveTilesH<F, CTW, PTW>;
     constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
@@ -855,6 +858,7 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     PHASE(2);
     PASS_NOW(tp2);
     PASS_ADD(1, tp2 - tp0);   // stem + tower
+    hook();                   // the caller's loads that may land during the head convs
     // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
     if (HEPI && n_blocks > 0) {   // the channel-group partials of the last epilogue, + bias, ReLU
         constexpr int CELLS = BS * BS, CG = WT::CG;

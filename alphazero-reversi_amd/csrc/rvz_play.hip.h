@@ -281,6 +281,12 @@ __device__ unsigned long long g_play_t[16384][12];
 #ifndef RVZ_PLAY_SPLIT_LAST
 #define RVZ_PLAY_SPLIT_LAST 0
 #endif
+// RVZ_PLAY_HEADS_PRE (bit 0: value fc1, bit 1: policy fc): those FC heads' weight loads are
+// issued by the cycle's last trunk pass before its 1x1 head convs, so they land while those run
+// (k_play waited ~6.3k cycles per cycle for them: profiles/r04f_play_phases_table1.json)
+#ifndef RVZ_PLAY_HEADS_PRE
+#define RVZ_PLAY_HEADS_PRE 0
+#endif
 // RVZ_PLAY_TOWER_PRIO (experiments): s_setprio for the evaluation phase (the trunk passes), 0
 // for the search and the FC heads
 #ifndef RVZ_PLAY_TOWER_PRIO
@@ -594,7 +600,26 @@ void k_play(PlayCtx ctx0) {
 #pragma unroll
                 for (int k = 0; k < NBOARD; ++k) gb[k] = q_rows[p0 + k];
                 const int t = opaque_tid();
-                if constexpr (HLDS)
+                if constexpr (HLDS && RVZ_PLAY_HEADS_PRE) {
+                    // the last pass of the cycle issues the FC heads' weight loads before its head
+                    // convs, and the heads run in the same iteration (no register lives across
+                    // the loop's back edge)
+                    const bool last = p0 + NBOARD >= nq;
+                    HeadsW<BS, RVZ_PLAY_HEADS_PRE> hw;
+                    h2_pass<F, NBOARD, CTW, PTW, BS, HeadsInLds<BS>, H2Def, BarWG>(
+                        smem, a.x, gb, q_bits + 3 * p0, a.prm, a.L, a.blob, a.n_blocks,
+                        HeadsInLds<BS>{hin, p0, nq}, t, t & 63,
+                        __builtin_amdgcn_readfirstlane(t >> 6), ovf, BarWG{}, [&] {
+                            if (last) hw.load(play_ctx().a.prm, play_ctx().a.L, opaque_tid());
+                        });
+                    if (last) {
+                        __syncthreads();
+                        const PlayArgs& a2 = play_ctx().a;
+                        heads_fc16<BS, HeadRowsList, false, false, GMAX, BarWG, RVZ_PLAY_HEADS_PRE>(
+                            a2.work, HeadRowsList{q_rows}, a2.prm, a2.L, a2.logits, a2.value, hin,
+                            vpart, opaque_tid(), BarWG{}, &hw);
+                    }
+                } else if constexpr (HLDS)
                     h2_pass<F, NBOARD, CTW, PTW, BS>(
                         smem, a.x, gb, q_bits + 3 * p0, a.prm, a.L, a.blob, a.n_blocks,
                         HeadsInLds<BS>{hin, p0, nq}, t, t & 63,
@@ -613,7 +638,7 @@ void k_play(PlayCtx ctx0) {
             PT_ADD(1, t_c3 - t_c2);
             PT_ADD(5, (nq + NBOARD - 1) / NBOARD);
             PT_ADD(6, nq);
-            for (int h0 = 0; h0 < nq; h0 += 16) {
+            for (int h0 = 0; h0 < nq && !(HLDS && RVZ_PLAY_HEADS_PRE); h0 += 16) {
                 const PlayArgs& a = play_ctx().a;
                 if constexpr (HLDS)   // the rows are in hin already (HeadsInLds); columns >= 8 mirror 0-7
                     heads_fc16<BS, HeadRowsList, false, false, GMAX>(
