@@ -1005,16 +1005,8 @@ __global__ __launch_bounds__(256) void k_autoreset(View v, const int32_t* __rest
 }
 
 #include "rvz_play.hip.h"
-// RVZ_PLAY12_BUILD 1 (experiments, tools/exp_play12.py): the team-specialised fused kernel
-// k_play12 (rvz_play12.hip.h), selected at run time by the env RVZ_PLAY_TEAMS=1. Measured equal
-// to k_play built with the same (H2Diet) trunk and 4% behind the default k_play (r04x, DESIGN
-// §8.6): not in the product library.
-#ifndef RVZ_PLAY12_BUILD
-#define RVZ_PLAY12_BUILD 0
-#endif
-#if RVZ_PLAY12_BUILD
-#include "rvz_play12.hip.h"
-#endif
+// (The team-specialised fused kernel k_play12 of round 4 — measured 4% behind k_play, DESIGN
+// §8.6 — is kept as tools/patches/play12_teams.patch, not in the product library.)
 
 // ---- board kernels on caller arrays (one thread per board) --------------------------------------
 template <int BS>
@@ -1813,32 +1805,6 @@ int rvz_play_timing_read(uint64_t* host, int n) {
 }
 #endif
 
-#if RVZ_PLAY12_BUILD
-// k_play12 (rvz_play12.hip.h): one 12-wave workgroup per CU, queue schedule only
-extern "C++" {
-template <int F, int NB, int CTW, int PTW, int BS>
-static int play12_launch(rvz_engine* e, const View& v, const PlayArgs& pa) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->cfg.device) !=
-            hipSuccess || cus <= 0)
-        cus = 256;
-    PlayArgs a = pa;
-    if (a.gpw <= 0) a.gpw = RVZ_PLAY_GROUP;
-    if (a.gpw > T12_SG) a.gpw = T12_SG;
-    a.n_groups = (v.G + a.gpw - 1) / a.gpw;
-    RVZ_HIP(fill32_async(a.q_next, 0u, (size_t)play_qwords(v.G), e->stream), e);
-    PlayCtx ctx;
-    ctx.v = v;
-    ctx.a = a;
-    hipLaunchKernelGGL((k_play12<F, NB, CTW, PTW, BS>), dim3(cus), dim3(768), 0, e->stream, ctx);
-    return launch_check(e, "k_play12");
-}
-}  // extern "C++"
-static bool play_teams_on() {
-    const char* t = getenv("RVZ_PLAY_TEAMS");
-    return t ? atoi(t) != 0 : RVZ_PLAY_TEAMS != 0;
-}
-#endif
 
 int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     const Range trace_range("rvz.play (fused search + h2 evaluator)");
@@ -1937,10 +1903,6 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.spin_limit = 1u << 26;
     if (const char* sl = getenv("RVZ_PLAY_SPIN_LIMIT")) pa.spin_limit = (unsigned)strtoul(sl, nullptr, 10);
     e->searching = 0;
-#if RVZ_PLAY12_BUILD
-    if (queue && e->BS == 8 && a->filters == 64 && play_teams_on())
-        return play12_launch<64, 2, 2, 4, 8>(e, v, pa);
-#endif
     if (e->BS == 8)
         return a->filters == 64 ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)
                                 : play_launch<128, 1, 2, 4, 8, 2>(e, v, pa, 2);

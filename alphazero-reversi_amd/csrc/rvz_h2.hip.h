@@ -63,10 +63,7 @@ constexpr int H2_K = 32, H2_TM = 16, H2_TN = 16;
 
 __host__ __device__ inline int64_t h2_layer_elems(int F) { return (int64_t)9 * F * F * 2; }
 __host__ __device__ inline int64_t h2_kstep_elems(int F) { return (int64_t)2 * F * H2_K; }
-// zero k-steps after the last layer: the weight prefetch of the next (absent) layer reads them.
-// (A mirrored wave (ILV) starts a layer at tap 8; its prefetch past the last layer lands in the
-// stem / scale words or past the blob, where the buffer descriptor's range check returns 0: the
-// values are discarded either way.)
+// zero k-steps after the last layer: the weight prefetch of the next (absent) layer reads them
 __host__ __device__ inline int64_t h2_pad_ksteps(int) { return 4; }
 static_assert(RVZ_H2_PD <= 4, "prefetch stays inside the padded blob");
 __host__ __device__ inline int64_t h2_stem_off(int F, int NB) {
@@ -176,7 +173,7 @@ struct WaveTilesH {
 
 // Weight fragments are read through a buffer descriptor over the whole blob: the wave-uniform
 // part of the address (layer, tap, k-step, part, channel tile) is the scalar soffset and the
-// lane's 16-byte slot the only VGPR, so a mirrored wave's runtime tap order costs scalar adds.
+// lane's 16-byte slot the only VGPR.
 // Reads past the blob return 0 (the descriptor's range check).
 struct H2W {
     __amdgpu_buffer_rsrc_t r;
@@ -189,79 +186,23 @@ struct H2W {
     }
 };
 // f16x8 index of k-step `it` of a layer (it >= NIT: the next layer's) from the layer's base:
-// [tap][kstep][part][ctile][lane]. mirror (ILV pixel group 1, RVZ_H2_MIRROR 1 or 2): the wave
-// walks the tap rows in reverse, so both groups meet their edge taps at the same it.
-#ifndef RVZ_H2_MIRROR
-#define RVZ_H2_MIRROR 0      // 0: natural order, a skip window per pixel group (conv_h2);
-#endif                       // 1: (dr, dc) -> (-dr, -dc); 2: rows only, (dr, dc) -> (-dr, dc)
-// the natural tap a mirrored wave reads at iteration tap t
-__host__ __device__ constexpr int h2_mirror_tap(int t) {
-    return RVZ_H2_MIRROR == 1 ? 8 - t : (2 - t / 3) * 3 + t % 3;
-}
+// [tap][kstep][part][ctile][lane]
 template <int F>
-__device__ __forceinline__ int h2_frag(int it, bool mirror) {
+__device__ __forceinline__ int h2_frag(int it) {
     constexpr int KS = F / H2_K, NIT = 9 * KS, CT = F / H2_TM, KSTEP = 2 * CT * 64;
     const int lay = it / NIT, itn = it % NIT, t = itn / KS, ks = itn % KS;
-    const int tn = mirror ? h2_mirror_tap(t) : t;
-    return (lay * NIT + tn * KS + ks) * KSTEP;
+    return (lay * NIT + t * KS + ks) * KSTEP;
 }
 
-// RVZ_H2_SKIP_LDS 1: the skip input is re-read from LDS as its two parts (x0 + x1, 22 bits: the
-// precision the conv inputs already carry; tools/emu_split.py f16x2_1acc_lds) at the place conv B
-// overwrites it, instead of kept in 32 fp32 registers. With the mirrored tap order (216 vs 248
-// VGPRs) that let a k_step or FC-heads wave (<= 80) share a SIMD with the two trunk waves:
-// +0.9-1.6% per ply (profiles/r02s_ablib_skiplds.txt, r02u). Under the natural-order trunk
-// (190 vs 220 VGPRs) the registers win: 0 (default) is +1.05% per ply
-// (profiles/r02ap_ab_skipreg.txt); `k_act` (63) still fits beside two 220-VGPR waves, k_step and
-// the heads capped at 72 measured the same (profiles/r02aq_ab_caps.txt).
-#ifndef RVZ_H2_SKIP_LDS
-#define RVZ_H2_SKIP_LDS 0
-#endif
-// RVZ_H2_W128 1: the epilogue stores 16 bytes per lane (ds_write_b128, one per tile) after a
-// v_permlane16_swap exchange between lane quads, instead of two 8-byte stores (ds_write_b64),
-// which are 2-way bank-conflicted in any slot swizzle: a 16-lane ds_write_b64 group is 16 pixels
-// of one channel quad, which fill only 8 of the 16 8-byte bank positions modulo 32 banks. Eight
-// contiguous lanes of a b128 store are 8 consecutive pixel rows of one part, whose slots
-// (row mod 2, (row >> 1) & 3) cover the 32 banks once: conflict-free (tools/lds_banks.py).
-// C2's geometry only (ILV: F = 64, two 8x8 boards; the callers pass W128 = RVZ_H2_W128 && ILV):
-// at F = 128 and for three 6x6 boards the exchange's live registers push k_play from 256 / 255
-// VGPRs into spills. Measured and NOT kept (r04n, profiles/r04n_*): k_play's LDS bank conflicts
-// 10.7% -> 0.7% of LDS cycles, but C2 -0.8% on one box (3 alternating pairs, 1,042.4k vs
-// 1,034.1k; 233 -> 239 VGPRs, +2.8% VALU): a 2-way ds_write_b64 costs 8 LDS-array cycles against
-// its ~6 transfer cycles, while the swaps and the 13-cycle b128 transfer cost more.
-#ifndef RVZ_H2_W128
-#define RVZ_H2_W128 0
-#endif
-// RVZ_H2_PK 1: the epilogue's scale + bias fma and residual add on channel pairs (packed fp32
-// VALU), per element the same operations in the same order. Measured and NOT kept (r04u,
-// profiles/r04u_ab_pk.txt): the conv epilogue drops from ~144-194 to ~129-174 VALU instructions
-// per wave, k_play 233 -> 235 VGPRs, C2 -0.3% on one box (3 alternating pairs): the epilogue's
-// VALU already issues in the partner's MFMA shadow.
-#ifndef RVZ_H2_PK
-#define RVZ_H2_PK 0
-#endif
-// The trunk's register / prefetch knobs as a type (the fused kernels instantiate more than one):
-// SKIP = RVZ_H2_SKIP_LDS, APD / PD = the activation / weight prefetch distances in k-steps
-// LATE: the epilogue's bias and inverse scales are loaded after the k-loop instead of before it
-// (16 fewer VGPRs held through the loop; the load's latency is then exposed at each epilogue)
-template <bool SKIP_, int APD_, int PD_, bool LATE_ = false>
-struct H2Knobs {
-    static constexpr bool SKIP = SKIP_, LATE = LATE_;
-    static constexpr int APD = APD_, PD = PD_;
-    static_assert(PD_ >= 1 && PD_ <= 4 && APD_ >= 0, "prefetch distances");
-};
-#ifndef RVZ_H2_LATE_EPI
-#define RVZ_H2_LATE_EPI 0
-#endif
-using H2Def = H2Knobs<RVZ_H2_SKIP_LDS != 0, RVZ_H2_APD, RVZ_H2_PD, RVZ_H2_LATE_EPI != 0>;
-// the trunk at <= 168 VGPRs (three waves per SIMD): skip input from LDS, no activation prefetch,
-// weights one k-step ahead (profiles/r04v_ab_trunk_register_diet.json: 166 VGPRs, 3.8% slower
-// alone)
-using H2Diet = H2Knobs<true, 0, 1>;
+// The skip input of a residual block stays in fp32 registers (EpiH::res) from conv A's epilogue
+// to conv B's. (Re-reading it from LDS as its two parts let a k_step or FC-heads wave share a SIMD
+// with two trunk waves under an earlier tap order; under the natural-order trunk the registers
+// win: +1.05% per ply, profiles/r02ap_ab_skipreg.txt.) Rejected epilogue / knob variants are
+// kept as patches in tools/patches/ (README there).
 template <int CTW, int PTW>
 struct EpiH {
     f32x4 bias[CTW], isc[CTW];       // per out-channel bias, inverse weight scale
-    float res[CTW][PTW][4];          // the block input (fp32) of this lane's outputs (SKIP: unused)
+    float res[CTW][PTW][4];          // the block input (fp32) of this lane's outputs
 };
 
 template <int F, int CTW, int PTW>
@@ -278,57 +219,31 @@ __device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __rest
 
 // v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
 // channels of one pixel per tile -> two 8-byte writes
-template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP, bool W128 = false,
-          bool SKIP = RVZ_H2_SKIP_LDS != 0>
+template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP>
 __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                                             const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
                                             const WaveTilesH<F, CTW, PTW>& wt, int lane,
                                             bool& ovf) {
     using C = CfgH<F, NPIX>;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
 #pragma unroll
         for (int u = 0; u < PTW; ++u) {
             const int n0 = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
             const int o = C::at(wt.px[u], n0 / H2_K, (n0 % H2_K) >> 3) + (n0 & 4);
-            f16x4 s0, s1;
-            if (RES && SKIP) {
-                s0 = *reinterpret_cast<const f16x4*>(out + o);
-                s1 = *reinterpret_cast<const f16x4*>(out + C::PLANE + o);
-            }
             u32x2 d0, d1;
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf) {
                 f32x2 v;
-                if constexpr (RVZ_H2_PK && !SKIP) {
-                    // the same per-element fma, add and max on channel pairs (v_pk_fma_f32,
-                    // v_pk_add_f32: one instruction per two values)
-                    const int j0 = 2 * hf;
-                    v = __builtin_elementwise_fma(f32x2{acc[c][u][j0], acc[c][u][j0 + 1]},
-                                                  f32x2{er.isc[c][j0], er.isc[c][j0 + 1]},
-                                                  f32x2{er.bias[c][j0], er.bias[c][j0 + 1]});
-                    if (RES) v = v + f32x2{er.res[c][u][j0], er.res[c][u][j0 + 1]};
-                    v = f32x2{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f)};
-                    ovf |= v[0] >= 65520.0f;
-                    ovf |= v[1] >= 65520.0f;
-                    if constexpr (KEEP) {
-                        er.res[c][u][j0] = v[0];
-                        er.res[c][u][j0 + 1] = v[1];
-                    }
-                } else
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int j = 2 * hf + e;
                     float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]);
-                    if (RES) {
-                        if constexpr (SKIP) x += (float)s0[j] + (float)s1[j];
-                        else x += er.res[c][u][j];
-                    }
+                    if (RES) x += er.res[c][u][j];
                     x = fmaxf(x, 0.0f);
                     ovf |= x >= 65520.0f;
-                    if constexpr (KEEP && !SKIP) er.res[c][u][j] = x;
+                    if constexpr (KEEP) er.res[c][u][j] = x;
                     v[e] = x;
                 }
                 uint32_t h0, h1;
@@ -336,71 +251,8 @@ __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                 d0[hf] = h0;
                 d1[hf] = h1;
             }
-            if constexpr (W128) {
-                // lane quads 2k and 2k+1 (rows 2k, 2k+1 of 16 lanes) hold channels n8..n8+3 and
-                // n8+4..+7 of one pixel: v_permlane16_swap(d0, d1) moves the odd quad's part-0
-                // half into the even quad's d1 and the even quad's part-1 half into the odd
-                // quad's d0, so the even quad writes the 8 channels of part 0 and the odd quad
-                // those of part 1, 16 bytes each
-                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const auto r = __builtin_amdgcn_permlane16_swap(d0[i], d1[i], false, false);
-                    d0[i] = r[0];
-                    d1[i] = r[1];
-                }
-                const int q = lane >> 4, n8 = (wt.ct0 + c) * H2_TM + 8 * (q >> 1);
-                const int o8 = C::at(wt.px[u], n8 / H2_K, (n8 % H2_K) >> 3) + (q & 1) * C::PLANE;
-                *reinterpret_cast<u32x4*>(out + o8) = u32x4{d0[0], d0[1], d1[0], d1[1]};
-            } else {
-                *reinterpret_cast<u32x2*>(out + o) = d0;
-                *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
-            }
-        }
-}
-
-// RVZ_H2_HEADS_EPI 1: the last conv's epilogue computes the 1x1 head convs (policy 2, value 1
-// output channels) from its fp32 outputs in registers instead of storing them to LDS for
-// head_convs to read back: per lane, partial dot products over its 4 x CTW channels for each of
-// its PTW pixels, reduced over the four lane groups (shuffles) and, through LDS, over the
-// channel-group waves. Needs the skip input in registers (the output buffer holds the partials).
-#ifndef RVZ_H2_HEADS_EPI
-#define RVZ_H2_HEADS_EPI 0
-#endif
-struct HeadPart {          // the 1x1 head-conv weights (pol_w [2][F], val_w [F]) and LDS partials
-    const float* pol;
-    const float* val;
-    float* part;           // [channel group][3][NPIX]
-};
-template <int F, int NPIX, int CTW, int PTW>
-__device__ __forceinline__ void epilogue_heads(const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
-                                               const WaveTilesH<F, CTW, PTW>& wt, int wave,
-                                               int lane, const f32x4 (&hw)[3][CTW],
-                                               float* __restrict__ part, bool& ovf) {
-    constexpr int CG = WaveTilesH<F, CTW, PTW>::CG;
-    float ph[PTW][3];
-#pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-        ph[u][0] = ph[u][1] = ph[u][2] = 0.0f;
-#pragma unroll
-        for (int c = 0; c < CTW; ++c)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]) + er.res[c][u][j];
-                x = fmaxf(x, 0.0f);
-                ovf |= x >= 65520.0f;
-#pragma unroll
-                for (int o = 0; o < 3; ++o) ph[u][o] = fmaf(x, hw[o][c][j], ph[u][o]);
-            }
-    }
-#pragma unroll
-    for (int u = 0; u < PTW; ++u)
-#pragma unroll
-        for (int o = 0; o < 3; ++o) {
-            float v = ph[u][o];
-            v += __shfl_xor(v, 16);
-            v += __shfl_xor(v, 32);
-            if (lane < 16) part[((wave % CG) * 3 + o) * NPIX + wt.px[u]] = v;
+            *reinterpret_cast<u32x2*>(out + o) = d0;
+            *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
         }
 }
 
@@ -494,8 +346,8 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 #endif
     }
     STEM_T(5);
-    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>::NPIX, CTW, PTW, false, true,
-                RVZ_H2_W128 && ILV>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>::NPIX, CTW, PTW, false, true>(
+        out, acc, er, wt, lane, ovf);
 }
 
 // The stem from the leaves' bitboards (the fused self-play kernel: select_phase leaves each
@@ -547,53 +399,41 @@ __device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
 #pragma unroll
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
     mma3<CTW, PTW, 0, 2>(acc, a, w);
-    epilogue_h2<F, G::NPIX, CTW, PTW, false, true, RVZ_H2_W128 && ILV>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, G::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
 }
 
-template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0,
-          bool LASTH = false, class K = H2Def>
+template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                         const H2W& wr, int wl,   // layer base, f16x8 units
                                         const float* __restrict__ bias,
                                         const float* __restrict__ isc, int wave, int lane,
-                                        f16x8 (&bc)[K::PD][CTW][2], EpiH<CTW, PTW>& er,
-                                        bool& ovf, HeadPart hp = HeadPart{}) {
+                                        f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
+                                        bool& ovf) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     using C = CfgH<F, G::NPIX>;
-    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = K::PD, APD = K::APD;
+    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
     // ILV: tile 0 is board row 0 (pixel group 0) or row 7 (group 1), and the taps with dr = -1
     // (row 0) or dr = +1 (row 7) leave the boards for all its pixels: tile 0's A loads and MFMAs
     // are skipped in those k-steps (1/12 of the conv MFMAs).
-    // RVZ_H2_MIRROR 0 (default, NAT): both groups walk the taps in natural order, so the two waves
-    // of a channel group fetch the same weight fragments at about the same time (L1 hits), and
-    // each skips in its own window, group 0 in [0, 3 KS) (dr = -1), group 1 in [6 KS, 9 KS)
-    // (dr = +1), both compile-time: the kernel instantiates the whole trunk once per group (GRP)
-    // behind one wave-uniform branch (190 VGPRs; the same choice made per layer needed 224, per
-    // k-step 248). Whole-bench A/B, one box: +2.8% over the row mirror
-    // (profiles/r02ah_ab_nat.txt).
-    // RVZ_H2_MIRROR 2 (row mirror): group 1 walks the tap rows in reverse (dr -> -dr) so both
-    // groups skip in k-steps [0, 3 KS) and share fragments only in the middle tap row: -3.2%
-    // trunk against no skip (profiles/r02k_ab_h2_mirror_c2.json); 1 (full mirror) shares only
-    // the centre tap: -2.1%.
-    constexpr bool NAT = ILV && RVZ_H2_MIRROR == 0;
+    // Both groups walk the taps in natural order, so the two waves of a channel group fetch the
+    // same weight fragments at about the same time (L1 hits), and each skips in its own window,
+    // group 0 in [0, 3 KS) (dr = -1), group 1 in [6 KS, 9 KS) (dr = +1), both compile-time: the
+    // kernel instantiates the whole trunk once per group (GRP) behind one wave-uniform branch (190
+    // VGPRs; the same choice made per layer needed 224, per k-step 248). Whole-bench A/B, one box:
+    // +2.8% over a row-mirrored tap order in which both groups skip in the same window
+    // (profiles/r02ah_ab_nat.txt; the mirrored orders lose the shared fragment fetches:
+    // profiles/r02k_ab_h2_mirror_c2.json).
     const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
-    const bool mirror = ILV && !NAT && wave / WaveTilesH<F, CTW, PTW>::CG != 0;
     // is tile 0 skipped in k-step i (compile-time once the k-loop is unrolled)
     auto skip0 = [](int i) -> bool {
         if (!ILV) return false;
-        if (NAT) return GRP == 0 ? i < 3 * KS : (i >= 6 * KS && i < 9 * KS);
-        return i < 3 * KS;
+        return GRP == 0 ? i < 3 * KS : (i >= 6 * KS && i < 9 * KS);
     };
-    if constexpr (!K::LATE) load_epi(er, bias, isc, wt, lane);   // lands during the k-loop
+    load_epi(er, bias, isc, wt, lane);                // lands during the k-loop
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
     unsigned pmask[PTW];                              // valid taps in iteration order
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-        const unsigned m = G::taps(wt.px[u]);
-        pmask[u] = !mirror ? m
-                   : RVZ_H2_MIRROR == 1 ? __builtin_bitreverse32(m) >> 23
-                                        : ((m & 7u) << 6) | (m & 0x38u) | ((m >> 6) & 7u);
-    }
+    for (int u = 0; u < PTW; ++u) pmask[u] = G::taps(wt.px[u]);
     f32x4 acc[CTW][PTW];
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
@@ -601,7 +441,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
     const int wu = wl + wt.ct0 * 64;
     auto load_b = [&](f16x8 (&bq)[CTW][2], int it) {
-        const int f = wu + h2_frag<F>(it, mirror);
+        const int f = wu + h2_frag<F>(it);
 #pragma unroll
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
@@ -609,7 +449,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     };
     auto load_a = [&](f16x8 (&aq)[PTW][2], int it) {
         const int t = it / KS, ks = it - t * KS;
-        const int off = mirror ? G::tap_offset(h2_mirror_tap(t)) : G::tap_offset(t);
+        const int off = G::tap_offset(t);
 #pragma unroll
         for (int u = (skip0(it) ? 1 : 0); u < PTW; ++u) {
             const int nat = wt.px[u] + off;
@@ -653,21 +493,8 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
         for (int c = 0; c < CTW; ++c)
 #pragma unroll
             for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
-    if constexpr (K::LATE) load_epi(er, bias, isc, wt, lane);
     // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
-    if constexpr (LASTH) {
-        f32x4 hw[3][CTW];                             // the head convs' weights (L2, once)
-#pragma unroll
-        for (int c = 0; c < CTW; ++c) {
-            const int n = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
-            hw[0][c] = *reinterpret_cast<const f32x4*>(hp.pol + n);
-            hw[1][c] = *reinterpret_cast<const f32x4*>(hp.pol + F + n);
-            hw[2][c] = *reinterpret_cast<const f32x4*>(hp.val + n);
-        }
-        epilogue_heads<F, G::NPIX, CTW, PTW>(acc, er, wt, wave, lane, hw, hp.part, ovf);
-    } else
-        epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES, RVZ_H2_W128 && ILV, K::SKIP>(out, acc, er,
-                                                                                  wt, lane, ovf);
+    epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
 }
 
 // the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for
@@ -740,17 +567,13 @@ struct HeadsInLds {
 // bits is set, the bitboards bits[3 * b .. 3 * b + 2] = (P, O, V) (LDS). Output: the 1x1
 // head-conv rows through hout (HeadsGlobalIdx: row gb[b] of work; HeadsInLds: the FC heads' LDS
 // input rows).
-struct NoHook {
-    __device__ __forceinline__ void operator()() const {}
-};
-template <int F, int NBOARD, int CTW, int PTW, int BS, class HOut, class K = H2Def,
-          class Bar = BarWG, class Hook = NoHook>
+template <int F, int NBOARD, int CTW, int PTW, int BS, class HOut>
 __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
                                         const int (&gbv)[NBOARD], const uint64_t* bits,
                                         const float* __restrict__ prm, const Layout& L,
                                         const uint16_t* __restrict__ blob, int n_blocks,
-                                        const HOut& hout, int tid, int lane, int wave, bool& ovf,
-                                        const Bar& bar = Bar{}, const Hook& hook = Hook{}) {
+                                        const HOut& hout, int tid, int lane, int wave, bool& ovf) {
+    const BarWG bar{};
     using WT = WaveTilesH<F, CTW, PTW>;
     constexpr bool ILV = RVZ_H2_ILV && NBOARD == 2 && BS == 8 && PTW == 4 && WT::CG == 2;
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
@@ -772,19 +595,17 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     // (issuing the stem's loads before the first conv's weight prefetch measured neutral: the
     // stem's epilogue time is the partner workgroup's MFMAs sharing the SIMD, not a load wait)
     const H2W wr(blob, h2_blob_elems(F, n_blocks));
-    // from the weight prefetch to the last residual block; NAT (RVZ_H2_MIRROR 0): one instance
-    // per pixel group (its own tile-0 skip window), chosen by a wave-uniform branch
-    const bool grp1 = ILV && RVZ_H2_MIRROR == 0 && wave / WT::CG != 0;
-    constexpr bool HEPI = RVZ_H2_HEADS_EPI && !K::SKIP && ILV;   // C2 shape (F = 128 spilled)
+    // from the weight prefetch to the last residual block: ILV, one instance per pixel group
+    // (its own tile-0 skip window, conv_h2), chosen by a wave-uniform branch
+    const bool grp1 = ILV && wave / WT::CG != 0;
     auto trunk = [&](auto grp) {
         constexpr int GR = decltype(grp)::value;
-        f16x8 bc[K::PD][CTW][2];
+        f16x8 bc[RVZ_H2_PD][CTW][2];
         if (n_blocks > 0) {
             const int wu = WT(wave, lane).ct0 * 64;
-            const bool mirror = ILV && RVZ_H2_MIRROR != 0 && wave / WT::CG != 0;   // as conv_h2
 #pragma unroll
-            for (int s = 0; s < K::PD; ++s) {
-                const int f = wu + h2_frag<F>(s, mirror);
+            for (int s = 0; s < RVZ_H2_PD; ++s) {
+                const int f = wu + h2_frag<F>(s);
 #pragma unroll
                 for (int c = 0; c < CTW; ++c)
 #pragma unroll
@@ -825,29 +646,17 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
         }
         const int64_t LW = h2_layer_elems(F);
         const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
-        for (int blk = 0; blk < n_blocks - (HEPI ? 1 : 0); ++blk) {
+        for (int blk = 0; blk < n_blocks; ++blk) {
             const int l1 = 2 * blk, l2 = 2 * blk + 1;
-            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR, false, K>(actA, actB, wr, (int)(l1 * LW / 8),
-                                                          prm + L.res_b + (size_t)l1 * F,
-                                                          isc + l1 * F, wave, lane, bc, er, ovf);
+            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
+                                                             prm + L.res_b + (size_t)l1 * F,
+                                                             isc + l1 * F, wave, lane, bc, er, ovf);
             if (blk == 0) PHASE(5);
             bar();
             if (blk == 0) PHASE(6);
-            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, false, K>(actB, actA, wr, (int)(l2 * LW / 8),
-                                                         prm + L.res_b + (size_t)l2 * F,
-                                                         isc + l2 * F, wave, lane, bc, er, ovf);
-            bar();
-        }
-        if (HEPI && n_blocks > 0) {   // the last block: its conv B ends in the head convs
-            const int l1 = 2 * n_blocks - 2, l2 = 2 * n_blocks - 1;
-            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR, false, K>(actA, actB, wr, (int)(l1 * LW / 8),
-                                                          prm + L.res_b + (size_t)l1 * F,
-                                                          isc + l1 * F, wave, lane, bc, er, ovf);
-            bar();
-            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, true, K>(
-                actB, actA, wr, (int)(l2 * LW / 8), prm + L.res_b + (size_t)l2 * F, isc + l2 * F,
-                wave, lane, bc, er, ovf,
-                HeadPart{prm + L.pol_w, prm + L.val_w, reinterpret_cast<float*>(actA)});
+            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR>(actB, actA, wr, (int)(l2 * LW / 8),
+                                                            prm + L.res_b + (size_t)l2 * F,
+                                                            isc + l2 * F, wave, lane, bc, er, ovf);
             bar();
         }
     };
@@ -858,27 +667,10 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     PHASE(2);
     PASS_NOW(tp2);
     PASS_ADD(1, tp2 - tp0);   // stem + tower
-    hook();                   // the caller's loads that may land during the head convs
     // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
-    if (HEPI && n_blocks > 0) {   // the channel-group partials of the last epilogue, + bias, ReLU
-        constexpr int CELLS = BS * BS, CG = WT::CG;
-        const float* part = reinterpret_cast<const float*>(actA);
-        const HOut& hpv = hout;
-        for (int o = tid; o < NBOARD * 3 * CELLS; o += NTHR) {
-            const int c2 = o / (NBOARD * CELLS), rem = o % (NBOARD * CELLS);
-            const int b = rem / CELLS, cell = rem % CELLS;
-            const int px = G::row_of(b, cell);
-            float acc = 0.0f;
-#pragma unroll
-            for (int g = 0; g < CG; ++g) acc += part[(g * 3 + c2) * G::NPIX + px];
-            const float bias = c2 < 2 ? prm[L.pol_b + c2] : prm[L.val_b];
-            hpv.store(b, c2 * CELLS + cell, fmaxf(acc + bias, 0.0f));
-        }
-    } else {
-        head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA},
-                                                  reinterpret_cast<float*>(actB), prm, L, hout,
-                                                  tid, bar);
-    }
+    head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA},
+                                              reinterpret_cast<float*>(actB), prm, L, hout, tid,
+                                              bar);
 #ifdef RVZ_PLAY_TIMING
     {
         PASS_NOW(tp3);
@@ -888,13 +680,6 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
 #endif
 }
 
-// RVZ_H2_MAXV (experiments): cap the trunk's VGPRs so that a k_step wave (80) fits on a SIMD
-// beside two trunk waves (2 x 216 + 80 = 512)
-#ifdef RVZ_H2_MAXV
-#define RVZ_H2_VGPR_ATTR __attribute__((amdgpu_num_vgpr(RVZ_H2_MAXV)))
-#else
-#define RVZ_H2_VGPR_ATTR
-#endif
 // bits 52-55 of a workgroup's end stamp: the XCD it ran on (HW_REG_XCC_ID; bench.py --stamps-dump)
 __device__ __forceinline__ uint64_t stamp_xcc() {
     return (uint64_t)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 0xF) << 52;

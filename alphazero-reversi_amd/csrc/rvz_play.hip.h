@@ -73,15 +73,6 @@ __host__ __device__ constexpr int play_gpw_max() {
 // game flags: a row queued for the NN, its output ready for the expand, the game's plies done,
 // its row in this cycle's passes, its row held back last cycle (an odd row waits one cycle)
 enum : int { PF_QUEUED = 1, PF_READY = 2, PF_DONE = 4, PF_EVAL = 8, PF_HELD = 16 };
-// RVZ_PLAY_BALANCE 1: a search phase deals the games that take a turn (neither queued nor done)
-// round-robin over the waves from a list built before it, instead of game j to wave j % 4: a
-// group of 6 gives waves 0 and 1 two games each only when more than 4 games take a turn.
-// Measured neutral (C2 1.1022M vs 1.1022M, C5 4.196M vs 4.194M, 3 + 2 alternating pairs,
-// profiles/r04k_ab_balance.txt): the partner workgroup's tower fills the SIMD while a search
-// phase runs, so a shorter one buys nothing. Off (the validated order).
-#ifndef RVZ_PLAY_BALANCE
-#define RVZ_PLAY_BALANCE 0
-#endif
 constexpr int32_t ERR_SCHED = 16;   // a queue wait timed out (device error word)
 
 // ---- the cross-game NN-output table (rvz_play_table) ---------------------------------------
@@ -272,26 +263,9 @@ __device__ unsigned long long g_play_t[16384][12];
 #define PT_ADD(i, v)
 #endif
 
-// RVZ_PLAY_SPLIT_LAST 1: the task queue's last ply is drawn as two tasks per group (its first
-// ceil(gpw / 2) games and the rest): a launch's end tail, where workgroups finish their last
-// tasks at spread-out times, is one half task instead of one task long. The games are the same
-// (a game's computation does not depend on which games share its task). Measured and NOT kept
-// (r04w, profiles/r04w_ab_split_last_*.txt): C2 -0.5% (20 plies) / -0.1% (60 plies) on one box:
-// a half task of 3 games runs fewer rows per pass and cycle than it saves in the tail.
-#ifndef RVZ_PLAY_SPLIT_LAST
-#define RVZ_PLAY_SPLIT_LAST 0
-#endif
-// RVZ_PLAY_HEADS_PRE (bit 0: value fc1, bit 1: policy fc): those FC heads' weight loads are
-// issued by the cycle's last trunk pass before its 1x1 head convs, so they land while those run
-// (k_play waited ~6.3k cycles per cycle for them: profiles/r04f_play_phases_table1.json)
-#ifndef RVZ_PLAY_HEADS_PRE
-#define RVZ_PLAY_HEADS_PRE 0
-#endif
-// RVZ_PLAY_TOWER_PRIO (experiments): s_setprio for the evaluation phase (the trunk passes), 0
-// for the search and the FC heads
-#ifndef RVZ_PLAY_TOWER_PRIO
-#define RVZ_PLAY_TOWER_PRIO 0
-#endif
+// Rejected schedule / phase variants (measured, not kept: dealing the search phase's games
+// round-robin, the last ply split into half tasks, the FC heads' weights loaded before the last
+// pass's head convs, s_setprio for the tower) are patches in tools/patches/ (README there).
 template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_play(PlayCtx ctx0) {
@@ -317,11 +291,9 @@ void k_play(PlayCtx ctx0) {
     __shared__ uint64_t q_bits[(GMAX + NBOARD) * 3];    // the same, in this cycle's row order
     __shared__ __attribute__((aligned(16))) float hin[HLDS ? GMAX * HROW : 4];   // heads rows
     __shared__ int q_rows[GMAX + 16];
-    __shared__ int s_act[GMAX];   // the games taking a turn in the next search phase
-    __shared__ int s_nact;
     __shared__ int s_nq;
     __shared__ float vpart[4][16];
-    __shared__ int s_task[3];
+    __shared__ int s_task[2];
     __shared__ unsigned s_tgen;
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -332,8 +304,7 @@ void k_play(PlayCtx ctx0) {
         G = c.v.G;
         gpw = c.a.gpw;
         queue = c.a.q_next != nullptr;
-        // RVZ_PLAY_SPLIT_LAST: the last ply's tasks are half groups (2 n_groups tasks)
-        total = queue ? c.a.n_groups * (c.a.plies + (RVZ_PLAY_SPLIT_LAST ? 1 : 0)) : 0;
+        total = queue ? c.a.n_groups * c.a.plies : 0;
         task_plies = queue ? 1 : c.a.plies;
     }
     bool ovf = false;
@@ -348,7 +319,7 @@ void k_play(PlayCtx ctx0) {
     PT_NOW(t_start);
     for (int task_i = 0;; ++task_i) {
         // ---- the next task: a game group and the ply it starts at
-        int gi, ply0, half = -1;
+        int gi, ply0;
         if (!queue) {
             if (task_i > 0) break;
             gi = blockIdx.x;
@@ -366,17 +337,10 @@ void k_play(PlayCtx ctx0) {
                     failed ? (unsigned)total
                            : __hip_atomic_fetch_add(a.q_next, 1u, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
-                int tg = -1, tp = 0, th = -1;
+                int tg = -1, tp = 0;
                 if ((int)t < total) {
-                    const unsigned full = (unsigned)a.n_groups * (unsigned)(a.plies - 1);
-                    if (RVZ_PLAY_SPLIT_LAST && t >= full) {   // a half of group tg, last ply
-                        tg = (int)((t - full) >> 1);
-                        th = (int)((t - full) & 1u);
-                        tp = a.plies - 1;
-                    } else {
-                        tg = (int)(t % (unsigned)a.n_groups);
-                        tp = (int)(t / (unsigned)a.n_groups);
-                    }
+                    tg = (int)(t % (unsigned)a.n_groups);
+                    tp = (int)(t / (unsigned)a.n_groups);
                     // the group's previous ply: played (and published) by the workgroup that
                     // drew it n_groups tasks ago, which is running; bounded spin, abandoned as
                     // soon as another workgroup's wait timed out
@@ -400,27 +364,17 @@ void k_play(PlayCtx ctx0) {
                 }
                 s_task[0] = tg;
                 s_task[1] = tp;
-                s_task[2] = th;
             }
             __syncthreads();   // the other waves load the group's state after the acquire
             gi = __builtin_amdgcn_readfirstlane(s_task[0]);
             ply0 = __builtin_amdgcn_readfirstlane(s_task[1]);
-            half = RVZ_PLAY_SPLIT_LAST ? __builtin_amdgcn_readfirstlane(s_task[2]) : -1;
             if (gi < 0) break;
             PT_NOW(t_q1);
             PT_ADD(8, t_q1 - t_q0);
             PT_ADD(9, 1);
         }
-        // half >= 0: games [h0, h0 + hn) of the group only (the last ply's half tasks)
-        const int h0 = half <= 0 ? 0 : (gpw + 1) / 2;
-        const int hn = half < 0 ? gpw : (half == 0 ? (gpw + 1) / 2 : gpw / 2);
-        const int g0 = gi * gpw + h0;
-        const int ng = min(hn, G - g0);
-        if (RVZ_PLAY_SPLIT_LAST && ng <= 0) {   // an empty half task (gpw 1, or the last group's second half)
-            if (!queue) break;
-            __syncthreads();   // every wave has read s_task before wave 0 draws the next task
-            continue;
-        }
+        const int g0 = gi * gpw;
+        const int ng = min(gpw, G - g0);
         {   // a game whose ply budget this task's ply reaches starts done
             const int32_t* bud = play_ctx().a.budget;
             for (int j = tid; j < ng; j += 256) {
@@ -428,21 +382,13 @@ void k_play(PlayCtx ctx0) {
                 st_f[j] = (bud && ply0 >= bud[g0 + j]) ? PF_DONE : 0;
                 st_p[j] = 0;
             }
-            if (RVZ_PLAY_BALANCE && tid == 0) {
-                int n = 0;
-                for (int j = 0; j < ng; ++j)
-                    if (!(bud && ply0 >= bud[g0 + j])) s_act[n++] = j;
-                s_nact = n;
-            }
         }
         __syncthreads();
         for (;;) {
             PT_NOW(t_c0);
             // search phase: each game not waiting for its row advances until it queues the next
             // row or has committed its plies (wave-uniform control flow per game)
-            const int n_turn = RVZ_PLAY_BALANCE ? __builtin_amdgcn_readfirstlane(s_nact) : ng;
-            for (int it = wave; it < n_turn; it += WPB) {
-                const int j = RVZ_PLAY_BALANCE ? __builtin_amdgcn_readfirstlane(s_act[it]) : it;
+            for (int j = wave; j < ng; j += WPB) {
                 const PlayCtx& c = play_ctx();
                 const View& v = c.v;
                 const PlayArgs& a = c.a;
@@ -591,35 +537,13 @@ void k_play(PlayCtx ctx0) {
             PT_NOW(t_c2);
 
             // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
-#if RVZ_PLAY_TOWER_PRIO
-            __builtin_amdgcn_s_setprio(RVZ_PLAY_TOWER_PRIO);   // experiments: tower over partner
-#endif
             for (int p0 = 0; p0 < nq; p0 += NBOARD) {
                 const PlayArgs& a = play_ctx().a;
                 int gb[NBOARD];
 #pragma unroll
                 for (int k = 0; k < NBOARD; ++k) gb[k] = q_rows[p0 + k];
                 const int t = opaque_tid();
-                if constexpr (HLDS && RVZ_PLAY_HEADS_PRE) {
-                    // the last pass of the cycle issues the FC heads' weight loads before its head
-                    // convs, and the heads run in the same iteration (no register lives across
-                    // the loop's back edge)
-                    const bool last = p0 + NBOARD >= nq;
-                    HeadsW<BS, RVZ_PLAY_HEADS_PRE> hw;
-                    h2_pass<F, NBOARD, CTW, PTW, BS, HeadsInLds<BS>, H2Def, BarWG>(
-                        smem, a.x, gb, q_bits + 3 * p0, a.prm, a.L, a.blob, a.n_blocks,
-                        HeadsInLds<BS>{hin, p0, nq}, t, t & 63,
-                        __builtin_amdgcn_readfirstlane(t >> 6), ovf, BarWG{}, [&] {
-                            if (last) hw.load(play_ctx().a.prm, play_ctx().a.L, opaque_tid());
-                        });
-                    if (last) {
-                        __syncthreads();
-                        const PlayArgs& a2 = play_ctx().a;
-                        heads_fc16<BS, HeadRowsList, false, false, GMAX, BarWG, RVZ_PLAY_HEADS_PRE>(
-                            a2.work, HeadRowsList{q_rows}, a2.prm, a2.L, a2.logits, a2.value, hin,
-                            vpart, opaque_tid(), BarWG{}, &hw);
-                    }
-                } else if constexpr (HLDS)
+                if constexpr (HLDS)
                     h2_pass<F, NBOARD, CTW, PTW, BS>(
                         smem, a.x, gb, q_bits + 3 * p0, a.prm, a.L, a.blob, a.n_blocks,
                         HeadsInLds<BS>{hin, p0, nq}, t, t & 63,
@@ -631,14 +555,11 @@ void k_play(PlayCtx ctx0) {
                         __builtin_amdgcn_readfirstlane(t >> 6), ovf);
                 __syncthreads();
             }
-#if RVZ_PLAY_TOWER_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
             PT_NOW(t_c3);
             PT_ADD(1, t_c3 - t_c2);
             PT_ADD(5, (nq + NBOARD - 1) / NBOARD);
             PT_ADD(6, nq);
-            for (int h0 = 0; h0 < nq && !(HLDS && RVZ_PLAY_HEADS_PRE); h0 += 16) {
+            for (int h0 = 0; h0 < nq; h0 += 16) {
                 const PlayArgs& a = play_ctx().a;
                 if constexpr (HLDS)   // the rows are in hin already (HeadsInLds); columns >= 8 mirror 0-7
                     heads_fc16<BS, HeadRowsList, false, false, GMAX>(
@@ -658,20 +579,8 @@ void k_play(PlayCtx ctx0) {
                         n_ins += tab_insert<BS>(a, s_tgen, P, O, Vb, opaque_tid() & 63, q_rows[i]);
                 }
             }
-            if (RVZ_PLAY_BALANCE) {   // flags, and the list of the next search phase's games
-                if (tid == 0) {
-                    int n = 0;
-                    for (int j = 0; j < ng; ++j) {
-                        int fj = st_f[j];
-                        if (fj & PF_EVAL) st_f[j] = fj = (fj & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
-                        if (!(fj & (PF_QUEUED | PF_DONE))) s_act[n++] = j;
-                    }
-                    s_nact = n;
-                }
-            } else {
-                for (int j = tid; j < ng; j += 256)
-                    if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
-            }
+            for (int j = tid; j < ng; j += 256)
+                if (st_f[j] & PF_EVAL) st_f[j] = (st_f[j] & ~(PF_QUEUED | PF_EVAL)) | PF_READY;
             __syncthreads();
             PT_NOW(t_c4);
             PT_ADD(2, t_c4 - t_c3);

@@ -15,7 +15,7 @@
 namespace {
 
 template <int F, int NBOARD, int CTW, int PTW, int BS, int OCC>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC))) RVZ_H2_VGPR_ATTR
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, OCC)))
 void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restrict__ prm,
                  Layout L, const uint16_t* __restrict__ blob, int n_blocks,
                  float* __restrict__ work, const int32_t* __restrict__ n_live,
@@ -30,9 +30,6 @@ void k_resnet_h2(const float* __restrict__ x, int n_boards, const float* __restr
     static_assert(1024 * 4 <= C::ACT * 2, "head-conv partial sums fit in B");
     static_assert(NBOARD * 100 * 4 * 4 <= C::ACT * 2, "xin fits in buffer B");
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
-#ifdef RVZ_H2_PRIO   // experiments: trunk waves ahead of co-resident search waves in issue
-    __builtin_amdgcn_s_setprio(RVZ_H2_PRIO);
-#endif
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int unit = blockIdx.x;
@@ -194,9 +191,6 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
     // the unit counter: words n*192 + 2, 3 of the workspace (8-byte aligned)
     unsigned long long* claim =
         RVZ_H2_DYN ? reinterpret_cast<unsigned long long*>(work + (size_t)n * 192 + 2) : nullptr;
-#ifndef RVZ_H2_DYN_LDS
-#define RVZ_H2_DYN_LDS 0      // extra dynamic LDS per workgroup (experiments: 1 workgroup per CU)
-#endif
     if (BS == 6) {   // packed 6x6: F=64 3 boards = 128 pixel rows (8 tiles); F=128 1 board = 48
         if (filters == 64)
             hipLaunchKernelGGL((k_resnet_h2<64, RVZ_H2_C5NB, 2, (RVZ_H2_C5NB * 36 + 31) / 32,
@@ -208,8 +202,8 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
                                params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
                                claim);
     } else if (filters == 64)
-        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), grid, dim3(256), RVZ_H2_DYN_LDS, s, x,
-                           n, params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
+        hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), grid, dim3(256), 0, s, x, n,
+                           params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
                            claim);
     else
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), grid, dim3(256), 0, s, x, n, params,

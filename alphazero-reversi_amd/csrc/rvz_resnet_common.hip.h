@@ -186,48 +186,13 @@ __host__ __device__ constexpr int heads_in_floats(int BS) {
 // (the fused kernel's head convs wrote them, HeadsInLds)
 // INROWS < 16: `in` holds INROWS rows and column c reads row c % INROWS (columns past the
 // rows are not stored: their outputs are discarded)
-// The FC heads' weight fragments of one wave (heads_fc16's non-streamed form), loadable ahead of
-// the heads (RVZ_PLAY_HEADS_PRE: k_play issues them before the last trunk pass's head convs)
-// MASK bit 0: the value fc1 fragments, bit 1: the policy fragments
-template <int BS, int MASK = 3>
-struct HeadsW {
-    static constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
-    static constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
-    static constexpr int PT = (POUT + 15) / 16, VJ = VK / 16, PJ = PK / 16, VTW = 256 / 16 / 4,
-                         PTW = (PT + 3) / 4;
-    f32x4 av[VTW][VJ], ap[PTW][PJ];
-    // every weight fragment of this wave's tiles: value fc1 tiles wave + 4m, policy tiles
-    // wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
-    __device__ __forceinline__ void load(const float* __restrict__ prm, const Layout& L, int tid) {
-        const int lane = tid & 63, wave = tid >> 6, col = lane & 15, grp = lane >> 4;
-#pragma unroll
-        for (int m = 0; m < VTW * (MASK & 1); ++m) {
-            const float* wr = prm + L.vfc1_w + (size_t)(16 * (wave + 4 * m) + col) * CELLS + 4 * grp;
-#pragma unroll
-            for (int j = 0; j < VJ; ++j)
-                av[m][j] = 16 * j + 4 * grp < CELLS ? *reinterpret_cast<const f32x4*>(wr + 16 * j)
-                                                    : f32x4{};
-        }
-#pragma unroll
-        for (int m = 0; m < PTW * (MASK >> 1 & 1); ++m) {
-            const int o = 16 * (wave + 4 * m) + col;
-            const float* wr = prm + L.pfc_w + (size_t)o * PIN + 4 * grp;
-#pragma unroll
-            for (int j = 0; j < PJ; ++j)
-                ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
-                               ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
-        }
-    }
-};
-
 template <int BS, class Rows, bool STREAM = RVZ_HEADS_STREAM != 0, bool COPY = true,
-          int INROWS = 16, class Bar = BarWG, int PRE = 0>
+          int INROWS = 16, class Bar = BarWG>
 __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const Rows& rmap,
                                            const float* __restrict__ prm, const Layout& L,
                                            float* __restrict__ logits, float* __restrict__ value,
                                            float* __restrict__ in, float (*vpart)[16],
-                                           int tid = threadIdx.x, const Bar& bar = Bar{},
-                                           const HeadsW<BS, PRE>* pre = nullptr) {
+                                           int tid = threadIdx.x, const Bar& bar = Bar{}) {
     constexpr int CELLS = BS * BS, PIN = 2 * CELLS, POUT = CELLS + 1;
     constexpr int VK = (CELLS + 15) / 16 * 16, PK = (PIN + 15) / 16 * 16;
     constexpr int PT = (POUT + 15) / 16, ROW = PK + VK + 4;   // +4: 16-B aligned, spread banks
@@ -273,18 +238,14 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
     // every weight fragment of this wave's tiles, issued before anything waits: value fc1 tiles
     // wave + 4m, policy tiles wave + 4m (A row = unit 16 t + col, k = 16 j + 4 grp .. +3)
     f32x4 av[VTW][VJ], ap[PTW][PJ];
-    // (PRE bit 0 / bit 1: the value / policy fragments were loaded ahead by the caller,
-    // HeadsW::load)
     if constexpr (!STREAM) {
 #pragma unroll
     for (int m = 0; m < VTW; ++m) {
         const float* wr = prm + L.vfc1_w + (size_t)(16 * (wave + 4 * m) + col) * CELLS + 4 * grp;
 #pragma unroll
         for (int j = 0; j < VJ; ++j)
-            if constexpr (PRE & 1) av[m][j] = pre->av[m][j];
-            else
-                av[m][j] = 16 * j + 4 * grp < CELLS ? *reinterpret_cast<const f32x4*>(wr + 16 * j)
-                                                    : f32x4{};
+            av[m][j] = 16 * j + 4 * grp < CELLS ? *reinterpret_cast<const f32x4*>(wr + 16 * j)
+                                                : f32x4{};
     }
 #pragma unroll
     for (int m = 0; m < PTW; ++m) {
@@ -292,10 +253,8 @@ __device__ __forceinline__ void heads_fc16(const float* __restrict__ work, const
         const float* wr = prm + L.pfc_w + (size_t)o * PIN + 4 * grp;
 #pragma unroll
         for (int j = 0; j < PJ; ++j)
-            if constexpr (PRE & 2) ap[m][j] = pre->ap[m][j];
-            else
-                ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
-                               ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
+            ap[m][j] = (o < POUT && 16 * j + 4 * grp < PIN)
+                           ? *reinterpret_cast<const f32x4*>(wr + 16 * j) : f32x4{};
     }
     }
 
