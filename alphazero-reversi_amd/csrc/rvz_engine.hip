@@ -1887,6 +1887,15 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     if (e->tab) {
         if (e->tab_blob != a->blob) {   // other weights than the generation's rows came from
             if (e->tab_blob) {
+                // the generation bump is a kernel on the stream: inside a capture it would be
+                // recorded and replayed, invalidating the table on every replay
+                hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+                if (hipStreamIsCapturing(e->stream, &cs) == hipSuccess &&
+                    cs != hipStreamCaptureStatusNone) {
+                    e->err = "rvz_play: another weight blob than the table's while the stream is "
+                             "capturing (play once eagerly with this evaluator before capturing)";
+                    return RVZ_EINVAL;
+                }
                 const int r = table_bump(e);
                 if (r != RVZ_OK) return r;
             }

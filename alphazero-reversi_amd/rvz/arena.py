@@ -227,19 +227,30 @@ class Arena:
         random.choice() from Python's (arena.py:178-180). So game k's draws are a contiguous
         piece of each stream, starting after everything games 0..k-1 drew.
 
-        Lockstep passes reproduce that exactly. A pass plays every game whose inputs changed
-        since the previous pass: its NumPy offset (the draws of the earlier games as the latest
-        pass counted them) and its Python generator state (the earlier games' choice() calls,
-        replayed in game order: a call's consumption depends only on len(seq)). A game's moves
-        are a function of those inputs alone (searches are per game, bit for bit), so a game
-        whose inputs did not change keeps its result. Game 0's inputs are exact from the start;
-        once games 0..k are exact, game k+1's inputs are, so the passes end (at most G + 1 of
-        them, two or three when only MCTS players meet: then the offsets depend only on the
-        earlier games' move counts). Both generators end where the sequential loop leaves them.
+        Lockstep passes reproduce that exactly. A game's inputs are its NumPy offset (the draws
+        of the earlier games as the latest pass counted them) and its Python generator state
+        (the earlier games' choice() calls replayed in game order from the arena's state); its
+        moves are a function of those inputs alone (searches are per game, bit for bit), so a
+        game whose inputs did not change keeps its result. A pass plays the games whose inputs
+        changed since they were last played, except that of the games with a random player only
+        the FIRST such changed game is played: its choice() calls set the generator state of
+        every later random-player game, so their replays in the same pass would be thrown away
+        (round 4 replayed them all: one pass per random-player game, each over the whole rest
+        of the tournament with full MCTS). Game 0's inputs are exact from the start,
+        and once games 0..k are exact, game k+1's are, so the passes end. Cost: MCTS-only
+        tournaments take two or three passes (the offsets depend only on the earlier games'
+        MCTS move counts, guessed right for most games); each game with a random player takes
+        one pass of its own (the reference plays every game one after another, and a random
+        game's generator state depends on the previous random game's moves), i.e. about
+        (random-player games + 2) passes, each as long as one game, with every other game
+        played about once. `reference_order_passes` reports the count; the engines are built
+        once per call. Both generators end where the sequential loop leaves them.
         """
         G = len(black_ids)
         nsq = self._board_size(black_ids, white_ids) ** 2
         mcts = {p: self.players[p].model is not None for p in set(black_ids) | set(white_ids)}
+        mcts_only = [mcts[black_ids[g]] and mcts[white_ids[g]] for g in range(G)]
+        cache: Dict = {}
         rs = np.random.RandomState()
         rs.set_state(self.np_rng.get_state())
         stream = rs.random_sample(G * (nsq - 4) + nsq)
@@ -260,16 +271,24 @@ class Arena:
                 for n in calls[g]:
                     r.choice(range(n))
             inputs = [(int(offsets[g]), states[g]) for g in range(G)]
-            todo = [g for g in range(G) if inputs[g] != prev[g]]
+            todo, rand_seen = [], False
+            for g in range(G):
+                if inputs[g] == prev[g]:
+                    continue
+                if not mcts_only[g]:          # one random-player game per pass (docstring)
+                    if rand_seen:
+                        continue
+                    rand_seen = True
+                todo.append(g)
             if not todo:
                 break
             draws = _ReferenceDraws(stream, offsets, states)
-            res = self._lockstep(black_ids, white_ids, todo, draws)
+            res = self._lockstep(black_ids, white_ids, todo, draws, cache=cache)
             for g in todo:
                 results[g] = res[g]
                 n_mcts[g] = draws.n_mcts[g]
                 calls[g] = draws.calls[g]
-            prev = inputs
+                prev[g] = inputs[g]
             self.reference_order_passes += 1
         total = int(sum(n_mcts))
         if total:
@@ -286,21 +305,26 @@ class Arena:
             raise ValueError(f"players of one batch play on one board size, got {sorted(sizes)}")
         return sizes.pop() if sizes else 8
 
-    def _lockstep(self, black_ids, white_ids, games, draws) -> List[Optional[float]]:
+    def _lockstep(self, black_ids, white_ids, games, draws,
+                  cache: Optional[Dict] = None) -> List[Optional[float]]:
         """Play `games` (indices into black_ids / white_ids) to their end in lockstep; the other
-        games start finished. draws supplies each MCTS move's uniform and each random move."""
+        games start finished. draws supplies each MCTS move's uniform and each random move.
+        cache: a dict that keeps the engines between calls over the same schedule."""
         G = len(black_ids)
         ids = sorted(set(black_ids) | set(white_ids))
         dev = next(iter(self.players[p].device for p in ids))
         bs = self._board_size(black_ids, white_ids)
         nsq = bs * bs
-        engines = {}
-        for pid in ids:
-            pl = self.players[pid]
-            if pl.model is not None:
-                engines[pid] = Engine(G, pl.num_simulations, pl.batch_size, pl.c_puct,
-                                      board_size=bs, device=dev, compact_leaves=True)
-        env = Engine(G, 64, 64, board_size=bs, device=dev)   # the authoritative boards (env only)
+        cache = {} if cache is None else cache
+        if not cache:
+            for pid in ids:
+                pl = self.players[pid]
+                if pl.model is not None:
+                    cache[pid] = Engine(G, pl.num_simulations, pl.batch_size, pl.c_puct,
+                                        board_size=bs, device=dev, compact_leaves=True)
+            cache[None] = Engine(G, 64, 64, board_size=bs, device=dev)   # the boards (env only)
+        engines = {pid: e for pid, e in cache.items() if pid is not None}
+        env = cache[None]
         env.reset(range(G))
         active = np.zeros(G, bool)
         active[list(games)] = True

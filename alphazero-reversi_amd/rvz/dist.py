@@ -142,6 +142,10 @@ def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2, kill_after_s: float
                 time.sleep(poll_s)
         return rc
     finally:
+        # a second SIGTERM during the cleanup must not raise out of it and strand live ranks
+        # (ADVICE r04): ignored until every child is gone, then the old handler is back
+        if old is not None:
+            signal.signal(signal.SIGTERM, signal.SIG_IGN)
         live = [p for p in procs if p.poll() is None]
         for p in live:
             p.terminate()
@@ -184,6 +188,32 @@ def barrier():
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
             dist.barrier()
+
+
+def gather(obj) -> list:
+    """Every rank's `obj` (picklable), in rank order, on every rank ([obj] without a group)."""
+    if not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def rank_report(local: dict, keys=("value", "seconds", "nn_rows_per_ply")) -> dict:
+    """Per-rank fields of a multi-rank measurement and their spread: `local` is this rank's dict
+    (its own rank, game range, plies, seconds, ...); returns {"per_rank": [dict per rank],
+    "spread": {key: {min, max, argmin, argmax, max_over_min}}} on every rank, so a slow or
+    unbalanced rank shows in the one JSON line instead of hiding in sum / max aggregates."""
+    ranks = gather(dict(local))
+    spread = {}
+    for k in keys:
+        vals = [(r.get(k), i) for i, r in enumerate(ranks) if isinstance(r.get(k), (int, float))]
+        if not vals:
+            continue
+        lo, hi = min(vals), max(vals)
+        spread[k] = {"min": lo[0], "max": hi[0], "argmin": lo[1], "argmax": hi[1],
+                     "max_over_min": round(hi[0] / lo[0], 4) if lo[0] else None}
+    return {"per_rank": ranks, "spread": spread}
 
 
 def aggregate_rate(local_units: float, local_seconds: float) -> Tuple[float, float, float]:

@@ -258,6 +258,10 @@ class Engine:
                                    or budget.device != self.device):
             raise RvzError("play: budget int32 [n_games] on the engine's device")
         rec = (None,) * 4
+        if records is not None and hist is None:
+            # the C-ABI's record contract: hist holds each recorded act's move (out_p is not
+            # written when records are given), so records without hist would lose the moves
+            raise RvzError("play: records need hist (the moves of the recorded plies)")
         if records is not None:
             rb, rw, rs, rp = records
             G = self.n_games

@@ -37,7 +37,11 @@ class SelfPlayTrainer:
                  weight_decay: float = 1e-4, gradient_clip: float = 1.0,
                  graph: bool = True, compact_leaves: bool = True, lr_milestones=(),
                  lr_gamma: float = 0.1, memo: bool = True, fused: bool = True,
-                 table_slots: int = 1 << 20, table_discs: int = 14):
+                 table_slots: Optional[int] = None, table_discs: int = 14):
+        """table_slots: slots of the fused launch's cross-game NN-output table (0: no table;
+        None: the next power of two >= 32 x games, within [2^12, 2^22]: 2^20 for C4's 32,768
+        games per rank). Each slot is 576 B of granules + a 4-B claim word on 8x8 (48 granules
+        on 6x6): 2^20 slots = 608 MB, 2^12 = 2.4 MB."""
         self.model = model.eval()
         self.device = next(model.parameters()).device
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -57,6 +61,8 @@ class SelfPlayTrainer:
         # memo's deferred last batch and the cross-game table (a new generation per refresh());
         # else the pull-style ply graph (per-batch launches, records copied per ply)
         self.fused = bool(fused)
+        if table_slots is None:
+            table_slots = 1 << min(22, max(12, (32 * self.games - 1).bit_length()))
         if self.fused and table_slots:
             self.eng.table(table_slots, table_discs)
         self.runner = SelfPlayRunner(self.eng, self.evaluator, temperature, record=True,

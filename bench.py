@@ -261,19 +261,38 @@ def setup(args):
 
 
 def dry_run(args, rank, world, backend):
+    """The launcher check without a GPU: ranks, process group, shards, and the per-rank report
+    of a real line (rvz.dist.rank_report) over a stand-in timed region (a short host loop per
+    rank, one "ply" per game of the shard), so the fields of the first N > 1 record are tested
+    on the CPU."""
     import torch.distributed as tdist
 
     from rvz import dist as rdist
     shards = [None] * world
     a, b = rdist.shard_range(args.games * world, rank, world)
     tdist.all_gather_object(shards, (rank, a, b, os.getpid()))
+    rdist.barrier()
+    t0 = time.perf_counter()
+    acc = 0
+    for g in range(a, b):                    # stand-in work, proportional to the shard
+        acc += sum(range(200)) + g
+    dt = max(time.perf_counter() - t0, 1e-9)
+    rep = rdist.rank_report(rank_fields(rank, a, b, b - a, dt, None, "cpu (dry run)"))
     if rank == 0:
         emit({"metric": "dry-run (launcher check)", "n_gpus": world, "rccl_world": world,
               "dist_backend": backend, "games_per_gpu": args.games,
               "global_games": args.games * world,
               "shards": [[r, a, b] for r, a, b, _ in shards],
-              "pids": sorted({p for *_, p in shards})})
+              "pids": sorted({p for *_, p in shards}), "ranks": rep})
     tdist.destroy_process_group()
+
+
+def rank_fields(rank, first_game, end_game, plies, seconds, rows_per_ply, device):
+    """One rank's part of a line: its global game range, committed plies, timed seconds, its own
+    rate and NN rows per ply (rvz.dist.rank_report gathers them and their spread)."""
+    return {"rank": rank, "games": [first_game, end_game], "plies": int(plies),
+            "seconds": round(seconds, 9), "value": round(plies / seconds, 2) if seconds > 0 else None,
+            "nn_rows_per_ply": rows_per_ply, "device": str(device), "pid": os.getpid()}
 
 
 # ------------------------------------------------------------------------------ measurement
@@ -734,6 +753,9 @@ def selfplay(args, device, rank, world, full=True):
     calls_per_search = [e.n_batches - (1 if args.skip_last_eval else 0) for e in engines]
     nn_calls = args.steps * sum(calls_per_search)
     rows = rows1 - rows0 if not args.no_compact else nn_calls * eng.n_games
+    # every rank's own plies, seconds, rate and rows per ply, and their spread (rank 0 prints)
+    ranks = rdist.rank_report(rank_fields(rank, first_game, first_game + args.games, s1 - s0,
+                                          t1 - t0, round(rows / max(1, s1 - s0), 3), device))
     trunk_live = None
     if graph_events:
         trunk_live = trunk_spans(graph_events[0], int(graph_events[1].item()))
@@ -796,7 +818,7 @@ def selfplay(args, device, rank, world, full=True):
             "timed_region_trunk_frac": round(region / peak, 4),
             "timed_region_useful_frac": round(upr * rows / (t1 - t0) / 1e12 / peak, 4)}
     plies_local = s1 - s0
-    out = {"value": value, "dt": dt, "total": total, "roofline": roof, "net": net,
+    out = {"value": value, "dt": dt, "total": total, "roofline": roof, "net": net, "ranks": ranks,
            "eng": eng, "ev": ev, "lanes": args.lanes,
            "nn_rows_per_ply": round(rows / max(1, plies_local), 3),
            "table": ({"slots": args.table_slots, "max_discs": args.table_discs,
@@ -933,6 +955,13 @@ def main_c4(args, rank, world, device):
     tr_s = rdist.reduce_max(sum(r["train_s"] for r in its))
     n_train = sum(r["steps"] for r in its)
     sp_rate = rdist.reduce_sum(steps) / sp_s
+    a0 = rank * args.games
+    loc = rank_fields(rank, a0, a0 + args.games, steps, t1 - t0,
+                      round(rows_sp / max(1, steps), 3) if args.fused else None, device)
+    loc["selfplay_s"] = round(sum(r["selfplay_s"] for r in its), 4)
+    loc["train_s"] = round(sum(r["train_s"] for r in its), 4)
+    ranks = rdist.rank_report(loc, keys=("value", "seconds", "selfplay_s", "train_s",
+                                         "nn_rows_per_ply"))
     # the gradient all-reduce alone: one flat fp32 bucket of every parameter (what DDP's single
     # 25 MB bucket carries), HIP events on the current stream, 20 back-to-back collectives
     buf = torch.randn(n_params, device=device)
@@ -1002,7 +1031,7 @@ def main_c4(args, rank, world, device):
                                             max(1, steps), 3),
                        "nn_rows_per_ply": round(rows_sp / max(1, steps), 3)}
                       if args.fused and args.table else None),
-            "selfplay_s": round(sp_s, 3), "train_s": round(tr_s, 3),
+            "selfplay_s": round(sp_s, 3), "train_s": round(tr_s, 3), "ranks": ranks,
             "ms_per_train_step": round(tr_s / max(1, n_train) * 1e3, 3),
             "allreduce": {"backend": tdist.get_backend(), "world": world,
                           "bytes": n_params * 4, "ms": round(ar_ms, 4),
@@ -1089,6 +1118,7 @@ def main():
                                  if args.table and args.fused else None),
                        "parallelism": f"games sharded x{world}"},
             "nn_rows_per_ply": r["nn_rows_per_ply"],
+            "ranks": r["ranks"],
             "table": r["table"],
             "nn_calls_per_ply": r["nn_calls_per_ply"],
             "host_enqueue_ms_per_step": r["host_enqueue_ms_per_step"],

@@ -232,8 +232,10 @@ int rvz_play(rvz_engine *e, const rvz_play_args *a);
  * engine. Visits, p and moves are identical with and without it (tests/test_gpu_table.py); it
  * changes how many rows are evaluated. Like the memo it requires unchanged weights:
  * rvz_search_memo_reset (new weights in place) starts a new table generation, and so does a call
- * of rvz_play with another weight blob. 8-byte {datum, generation} granules written and read with
- * agent-scope accesses, so workgroups on every XCD share it without fences. Not inside a search. */
+ * of rvz_play with another weight blob (a kernel on the stream: refused with RVZ_EINVAL while the
+ * stream is capturing, so a captured graph never replays it; play once eagerly per evaluator
+ * before capturing). 8-byte {datum, generation} granules written and read with agent-scope
+ * accesses, so workgroups on every XCD share it without fences. Not inside a search. */
 int rvz_play_table(rvz_engine *e, int64_t slots, int32_t max_discs);
 
 /* ---- introspection (tests / bench) -------------------------------------------------------- */

@@ -20,17 +20,18 @@ def test_elo_sequence_matches_reference(tmp_path):
     assert again.ratings == elo.ratings and again.games_played == elo.games_played
 
 
-def _fake_game(g, mcts_side, u_of, choice_of):
+def _fake_game(g, mcts_side, u_of, choice_of, mcts_ends=True):
     """A stand-in for one game's moves that consumes draws like an arena game: up to 12 moves,
-    sides alternate; an MCTS move takes one uniform and ends the game below 0.15, a random move
-    chooses among 1 + (7 t + g) mod 9 squares and ends the game on square 0. Returns a result
-    that depends on every draw."""
+    sides alternate; an MCTS move takes one uniform and (mcts_ends) ends the game below 0.15, a
+    random move chooses among 1 + (7 t + g) mod 9 squares and ends the game on square 0. Returns
+    a result that depends on every draw. mcts_ends False: an MCTS-only game always makes 12
+    moves, as 8x8 games (60 plies, 30 moves a side, bar passes) nearly always do."""
     h = 0
     for t in range(12):
         if mcts_side[t % 2]:
             u = u_of()
             h = (h * 31 + int(u * 1e6)) % 1000003
-            if u < 0.15:
+            if u < 0.15 and mcts_ends:
                 break
         else:
             m = choice_of(list(range(1 + (7 * t + g) % 9)))
@@ -49,7 +50,11 @@ def test_reference_draw_order_passes_reproduce_sequential_draws(monkeypatch):
     import numpy as np
     from rvz.arena import Arena
 
-    def fake_lockstep(self, black_ids, white_ids, games, draws):
+    played = []
+    ends = [True]
+
+    def fake_lockstep(self, black_ids, white_ids, games, draws, cache=None):
+        played.extend(games)
         G = len(black_ids)
         draws.begin_ply(G)
         res = [None] * G
@@ -57,13 +62,15 @@ def test_reference_draw_order_passes_reproduce_sequential_draws(monkeypatch):
             side = (self.players[black_ids[g]].model is not None,
                     self.players[white_ids[g]].model is not None)
             res[g] = _fake_game(g, side, lambda: float(draws.uniforms(np.array([g]))[g]),
-                                lambda sq: draws.choice(g, sq))
+                                lambda sq: draws.choice(g, sq), ends[0])
         return res
 
     monkeypatch.setattr(Arena, "_lockstep", fake_lockstep)
-    for pairs in ([("a", "b")] * 5, [("a", "r"), ("r", "b"), ("a", "b"), ("r", "r")] * 4,
-                  [("r", "r")] * 6):
+    mixed = [("a", "r"), ("r", "b"), ("a", "b"), ("r", "r")] * 4
+    for pairs, ends[0] in (([("a", "b")] * 5, True), (mixed, True), ([("r", "r")] * 6, True),
+                           ([("a", "b")] * 12, False), (mixed, False)):
         arena = Arena(seed=5)
+        played.clear()
         for pid in "abr":
             arena.players[pid] = types.SimpleNamespace(
                 model=None if pid == "r" else object(), board_size=8, device="cpu")
@@ -72,9 +79,16 @@ def test_reference_draw_order_passes_reproduce_sequential_draws(monkeypatch):
         got = arena.play_games(black, white)
         np_rng, py_rng = np.random.RandomState(5), random.Random(5)
         want = [_fake_game(g, (b != "r", w != "r"), lambda: float(np_rng.random_sample()),
-                           py_rng.choice) for g, (b, w) in enumerate(pairs)]
+                           py_rng.choice, ends[0]) for g, (b, w) in enumerate(pairs)]
         assert got == want
         assert arena.np_rng.random_sample() == np_rng.random_sample()
         assert arena.py_rng.random() == py_rng.random()
         assert arena.reference_order_passes <= len(pairs) + 1
-        print(pairs[:2], "passes", arena.reference_order_passes)
+        if not ends[0]:
+            # cost when MCTS move counts are fixed, as in real games: one pass per
+            # game with a random player plus at most three, and every game played a bounded
+            # number of times (round 4 replayed the whole rest of the tournament every pass)
+            n_rand = sum(1 for b, w in pairs if "r" in (b, w))
+            assert arena.reference_order_passes <= n_rand + 3
+            assert len(played) <= 3 * len(pairs), len(played)
+        print(pairs[:2], "passes", arena.reference_order_passes, "plays", len(played))

@@ -39,6 +39,31 @@ def test_bench_gpus_n_starts_n_ranks(n, games):
     assert len(d["pids"]) == n                  # n distinct processes
 
 
+def test_bench_world4_line_carries_per_rank_fields():
+    """a line of N > 1 ranks must show each rank's own plies,
+    seconds, rate, rows per ply and game range, and their spread (a slow rank would otherwise
+    hide in sum-over-max). The dry run fills the same report (rvz.dist.rank_report) from a
+    stand-in timed region."""
+    n, games = 4, 96
+    r = _run(["--gpus", str(n), "--dist-backend", "gloo", "--dry-run", "--games", str(games)])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    rep = d["ranks"]
+    per = rep["per_rank"]
+    assert [p["rank"] for p in per] == list(range(n))
+    assert [p["games"] for p in per] == [[k * games, (k + 1) * games] for k in range(n)]
+    assert len({p["pid"] for p in per}) == n
+    for p in per:
+        assert p["plies"] == games and p["seconds"] > 0
+        assert abs(p["value"] - p["plies"] / p["seconds"]) <= 1e-3 * p["value"]
+    for k in ("value", "seconds"):
+        sp = rep["spread"][k]
+        vals = [p[k] for p in per]
+        assert sp["min"] == min(vals) and sp["max"] == max(vals)
+        assert per[sp["argmin"]][k] == sp["min"] and per[sp["argmax"]][k] == sp["max"]
+        assert sp["max_over_min"] >= 1.0
+
+
 def test_bench_single_rank_forms_a_group_of_one():
     r = _run(["--dry-run", "--games", "64"])
     assert r.returncode == 0, r.stderr[-2000:]

@@ -83,12 +83,14 @@ def test_fused_workgroup_sizes_and_launch_splits(gpw, chunks):
           _plain(net, G, S, 20, True, True))
 
 
-@pytest.mark.parametrize("board,blocks,filters", [(8, 2, 128), (6, 2, 64), (6, 1, 128)])
-def test_fused_other_geometries(board, blocks, filters):
-    """The C3 trunk shape (128 filters, one board per pass) and the packed 6x6 geometry (C5)."""
+@pytest.mark.parametrize("board,blocks,filters,gpw", [(8, 2, 128, 0), (8, 2, 128, -16),
+                                                     (6, 2, 64, 0), (6, 1, 128, 0)])
+def test_fused_other_geometries(board, blocks, filters, gpw):
+    """The C3 trunk shape (128 filters, one board per pass; with the default queue groups and
+    with bench.py's C3 groups of 16, play_group -16) and the packed 6x6 geometry (C5)."""
     net = _net(board, blocks, filters, seed=1)
     G, S, plies = 160, 160 if board == 8 else 100, 24
-    _same(_fused(net, G, S, plies, True, True), _plain(net, G, S, plies, True, True))
+    _same(_fused(net, G, S, plies, True, True, gpw=gpw), _plain(net, G, S, plies, True, True))
 
 
 def test_fused_headline_configuration_at_full_size():

@@ -92,6 +92,41 @@ def test_k_play_c3_shape_vs_oracle_whole_games(oracle):
     _vs_oracle(oracle, net, 96, 800, 60, -4, sample_n=12)
 
 
+def test_k_play_c3_bench_form_at_full_size(oracle):
+    """C3 exactly as bench.py runs it: 32,768 games x 800 sims, the 10x128
+    net, memo + the last batch left to it + the cross-game table, the task queue with groups of
+    16 (play_group -16), autoreset; one k_play launch per ply. Every ply: 16 sampled games equal
+    the oracle (f64 policy bitwise, move), and every game's move equals the pull-style runner's
+    (per-batch launches, no table); at the end boards / statuses / counters / seeds / p equal."""
+    import rvz
+    net = _net(8, 10, 128)
+    G, S, plies = 32768, 800, 2
+    run = _fused_runner(net, G, S, gpw=-16, table=(1 << 20, 14))
+    ref = rvz.SelfPlayRunner(rvz.Engine(G, S, 64, compact_leaves=True, memo=True),
+                             rvz.LeafEvaluator(net), autoreset=True, seed_base=42,
+                             skip_last_eval=True)
+    ref.start()
+    sample = np.linspace(0, G - 1, 16).astype(int)
+    orc = OracleGames(oracle, [42 + int(g) for g in sample], S)
+    for ply in range(plies):
+        hist = _play(run, 1)
+        run.eng.check()
+        ref.ply()
+        assert torch.equal(hist[0], ref.eng.idx_buf), f"ply {ply}: fused != pull-style"
+        _, oi, op, _ = orc.ply(run.evaluator)
+        idx = hist[0].cpu().numpy()
+        p = run.eng.p_buf.cpu().numpy()
+        assert np.array_equal(oi, idx[sample]), (ply, oi, idx[sample])
+        assert np.array_equal(op.view(np.int64), p[sample].view(np.int64)), ply
+    for x, y in zip(run.eng.get_state(), ref.eng.get_state()):
+        assert torch.equal(x, y)
+    assert torch.equal(run._plies, ref._plies) and torch.equal(run._done, ref._done)
+    assert torch.equal(run.seeds, ref.seeds) and torch.equal(run.eng.p_buf, ref.eng.p_buf)
+    assert int(run.eng.table_stats[0].item()) > 0      # opening positions: table hits
+    ref.eng.check()
+    assert not run.evaluator.overflowed()
+
+
 def test_k_play_c5_preset_equals_runner_at_full_size():
     """C5 as bench.py runs it (16,384 games, 400 sims, groups of 24, three 6x6 boards per
     workgroup), 34 plies (every 6x6 game ends within 32, so restarts are included): every ply's

@@ -116,3 +116,51 @@ def test_table_generations_follow_the_weights():
         eng.check()
         out.append(torch.stack(moves))
     assert torch.equal(out[0], out[1])
+
+
+def test_table_blob_switch_is_refused_inside_a_capture():
+    """a play with another weight blob bumps the table generation with a kernel on
+    the stream; inside a graph capture that kernel would be recorded and invalidate the table on
+    every replay, so rvz_play refuses it there. After one eager play with the new evaluator the
+    capture goes through, and its replays keep the table (hits accumulate)."""
+    import rvz
+    G, S = 64, 96
+    eng = rvz.Engine(G, S, 64, memo=True)
+    eng.table(1 << 12, 14)
+    ev_a = rvz.LeafEvaluator(_net(8, 1, 64, seed=1))
+    ev_b = rvz.LeafEvaluator(_net(8, 1, 64, seed=2))
+    run = rvz.SelfPlayRunner(eng, ev_a, autoreset=True, seed_base=3, skip_last_eval=True,
+                             fused=True)
+    run.start()
+    run._body(2)                      # the table's generation belongs to ev_a's blob
+    eng.play_buffers(ev_b)
+    run.evaluator = ev_b
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(rvz.RvzError, match="capturing"):
+        with torch.cuda.graph(g):
+            run._body(1)
+    torch.cuda.synchronize()
+    run._body(1)                      # eager: the generation moves to ev_b's blob
+    run.capture(plies=1)
+    h0 = int(eng.table_stats[0].item())
+    for _ in range(3):
+        run.ply()
+    torch.cuda.synchronize()
+    eng.check()
+    assert int(eng.table_stats[0].item()) > h0
+
+
+def test_play_records_need_hist():
+    """the C-ABI writes a recorded act's move only to hist (out_p is not written
+    with records), so Engine.play refuses records without hist instead of losing the moves."""
+    import rvz
+    G, S, n = 16, 64, 2
+    eng = rvz.Engine(G, S, 64, memo=True)
+    ev = rvz.LeafEvaluator(_net(8, 1, 64))
+    z = torch.zeros(G, dtype=torch.int64, device="cuda")
+    rec = (torch.zeros(n, G, dtype=torch.int64, device="cuda"),
+           torch.zeros(n, G, dtype=torch.int64, device="cuda"),
+           torch.zeros(n, G, dtype=torch.int32, device="cuda"),
+           torch.zeros(n, G, eng.npol, dtype=torch.float64, device="cuda"))
+    with pytest.raises(rvz.RvzError, match="hist"):
+        eng.play(ev, n, 1.0, z + 5, G, z.clone(), z.clone(), records=rec)
