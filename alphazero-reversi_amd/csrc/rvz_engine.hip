@@ -1723,6 +1723,11 @@ int rvz_search_skip(rvz_engine* e) {
         return RVZ_EINVAL;
     }
     if (e->pending) { e->err = "rvz_search_skip after rvz_search_submit"; return RVZ_EINVAL; }
+    if (S <= B) {     // one batch: its leaf is the root, whose expansion the act needs
+        e->err = "rvz_search_skip needs a search of at least two batches (num_simulations > "
+                 "batch_size): a single batch's leaf is the root";
+        return RVZ_EINVAL;
+    }
     e->pending = 2;   // rvz_act: visit counts only
     return RVZ_OK;
 }
@@ -1855,7 +1860,9 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.ovf = a->ovf;
     pa.gpw = queue ? -a->games_per_workgroup : a->games_per_workgroup;
     pa.plies = a->plies;
-    pa.skip_last = a->skip_last_eval ? 1 : 0;
+    // a search of one batch (S <= B) evaluates it: its leaf is the root, which the act needs
+    // expanded (the deferred last batch is dead only from the second batch on)
+    pa.skip_last = a->skip_last_eval && e->cfg.num_simulations > e->cfg.batch_size ? 1 : 0;
     pa.reset = a->reset ? 1 : 0;
     pa.S = e->cfg.num_simulations;
     pa.B = e->cfg.batch_size;

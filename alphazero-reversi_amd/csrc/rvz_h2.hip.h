@@ -42,6 +42,7 @@ namespace {
 //   [H2_PAD k-steps of zeros: the prefetch past the last layer]
 //   [stem frags: part][ctile][lane][8]  (K = 27 padded to 32, k = tap*3 + ch)
 //   [inverse scales: float[1 + 2*NB][F]: stem, then the trunk layers]
+//   [activation ranges: float[1 + 2*NB][2] {K, Bb} (h2_range_off; ActRange below)]
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
@@ -72,8 +73,14 @@ __host__ __device__ inline int64_t h2_stem_off(int F, int NB) {
 __host__ __device__ inline int64_t h2_scale_off(int F, int NB) {   // uint16 units, 16-B aligned
     return h2_stem_off(F, NB) + (int64_t)2 * F * H2_K;
 }
-__host__ __device__ inline int64_t h2_blob_elems(int F, int NB) {
+// the activation-range table (uint16 units, 16-B aligned): float[1 + 2 NB][2] = per layer (stem,
+// then the trunk convs) {K = max over output channels of sum |w| (BN-folded, unscaled), Bb = max
+// |bias|}: a layer's outputs are bounded by K * max|input| + Bb (+ the skip input's max)
+__host__ __device__ inline int64_t h2_range_off(int F, int NB) {
     return h2_scale_off(F, NB) + (int64_t)2 * (1 + 2 * NB) * F;
+}
+__host__ __device__ inline int64_t h2_blob_elems(int F, int NB) {
+    return h2_range_off(F, NB) + ((int64_t)4 * (1 + 2 * NB) + 7) / 8 * 8;
 }
 
 // x == h0 + h1 + r, |r| <= 2^-22 |x| for |x| in the f16 normal range (round to nearest even)
@@ -102,6 +109,8 @@ struct GeoH {
     static constexpr int NVALID = NB * PPB;
     static constexpr int NPIX = (NVALID + RND - 1) / RND * RND;
     static constexpr int RS = ILV ? NB * BS : BS;    // pixel-row stride of a board row
+    static constexpr int NBRD = NB;
+    static constexpr bool ILVD = ILV;
     static_assert(!ILV || (NB == 2 && BS == 8), "interleaved rows: two 8x8 boards");
     static __device__ __forceinline__ int cell_of(int px) {
         return ILV ? (px >> 4) * 8 + (px & 7) : px % PPB;
@@ -130,7 +139,8 @@ struct CfgH {
     static constexpr int KSP = (ZROW + 8) * H2_K;    // halves per k-step plane
     static constexpr int PLANE = KS * KSP;           // halves per part
     static constexpr int ACT = 2 * PLANE;            // halves per buffer
-    static constexpr int BYTES = 2 * ACT * 2;
+    static constexpr int RMAX = 2 * ACT * 2;         // byte offset of the range maxima (RangeLds)
+    static constexpr int BYTES = RMAX + 3 * 4 * 4 * 4 + 16;  // + the pass's overflow word
     static constexpr int NIT = 9 * KS;
     static constexpr int CT = F / H2_TM;
     static_assert((PLANE * 2) % 16 == 0 && (KSP * 2) % 16 == 0, "16-byte aligned planes");
@@ -141,10 +151,94 @@ struct CfgH {
     }
 };
 
-// activation reader for the heads (join of the two parts)
+// ---- activation range ------------------------------------------------
+// The f16 parts of an activation overflow at 65520. Each board's image is therefore stored as
+// x * 2^-s, with s chosen per board and layer, before the layer's epilogue writes it, from a
+// bound on the layer's outputs: K * (the measured max of its input image) + Bb (+ the max of
+// the skip input), K = max over output channels of sum |w| and Bb = max |bias| from the blob's
+// range table (rvz_resnet_h2_weights). s = 0 while the bound stays below 2^15 — every random-init
+// and trained net measured — and then the stored image, the MFMAs and every output are bitwise
+// those of the unscaled kernel (the scaled path is a separate, wave-uniform branch). A scaled
+// board keeps fp32-class accuracy relative to its largest activation; values below 2^(s - 3)
+// lose low-order bits to f16 subnormals. The next layer's epilogue multiplies its accumulator by
+// 2^s (exact) before the bias. Maxima: each wave's per-board max of its true (unscaled) outputs
+// goes to LDS (RangeLds), where the next layer reads it after the barrier between the two.
+__device__ __forceinline__ int range_exp(float bound) {
+    if (!(bound < 0x1p100f)) return 100;             // inf / NaN weights: the image is lost anyway
+    int e = 0;
+    (void)frexpf(bound, &e);                         // bound < 2^e
+    return e > 15 ? e - 15 : 0;
+}
+__device__ __forceinline__ float pow2f(int s) {      // 2^s, |s| <= 126
+    return __int_as_float((127 + s) << 23);
+}
+// the max of a non-negative value over the wave, wave-uniform: DPP within rows of 16 lanes
+// (quad swaps, then row shifts by 4 and 8 with zero fill), then the four row maxima
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+    auto up = [](float x, auto ctrl) {
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x),
+                                                          decltype(ctrl)::value, 0xF, 0xF, true));
+    };
+    v = fmaxf(v, up(v, std::integral_constant<int, 0xB1>{}));    // quad_perm [1, 0, 3, 2]
+    v = fmaxf(v, up(v, std::integral_constant<int, 0x4E>{}));    // quad_perm [2, 3, 0, 1]
+    v = fmaxf(v, up(v, std::integral_constant<int, 0x114>{}));   // row_shr:4
+    v = fmaxf(v, up(v, std::integral_constant<int, 0x118>{}));   // row_shr:8: lane 15 of a row
+    auto rl = [&](int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); };
+    return fmaxf(fmaxf(rl(15), rl(31)), fmaxf(rl(47), rl(63)));
+}
+template <int NB>
+struct RangeS {                     // wave-uniform scale exponents of an image, 8 bits per board
+    int pk = 0;
+    __device__ int s(int k) const { return (pk >> (8 * k)) & 0xFF; }
+    __device__ bool any() const { return pk != 0; }
+    // 2^(sign * s(b)) for a lane's board b (b >= NB: padding rows, 1)
+    __device__ float mul(int b, int sign) const {
+        return b < NB ? pow2f(sign * ((pk >> (8 * b)) & 0xFF)) : 1.0f;
+    }
+};
+// maxima in LDS: [slot][board < 4][wave < 4] floats at CfgH::RMAX; slots 0 / 2 = the inputs of
+// even / odd residual blocks (the stem and conv B write them), 1 = conv A's outputs (and the
+// stem's input in the pull-style pass)
+struct RangeLds {
+    float* p;
+    __device__ float* slot(int par) const { return p + par * 16; }
+    // a wave's overflow word of the pass (bit b: board b stored a value past f16's range,
+    // unranged mode): one per wave, so each wave clears and sets its own in program order
+    __device__ unsigned* ovw(int wave) const { return reinterpret_cast<unsigned*>(p + 48) + wave; }
+    // the pass's overflow bits: every wave's word (after a barrier that follows their epilogues)
+    __device__ unsigned ov_all() const {
+        const unsigned* q = reinterpret_cast<const unsigned*>(p + 48);
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)(q[0] | q[1] | q[2] | q[3]));
+    }
+    // the max over the 4 waves of board b (wave-uniform)
+    __device__ float read(int par, int b) const {
+        const float* q = slot(par) + 4 * b;
+        const float m = fmaxf(fmaxf(q[0], q[1]), fmaxf(q[2], q[3]));
+        return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__float_as_int(m)));
+    }
+};
+// the output scale exponents of a layer from its bound, per board
+template <int NB>
+__device__ __forceinline__ RangeS<NB> range_out(const float (&m_in)[NB], float K, float Bb,
+                                               const float* m_skip) {
+    RangeS<NB> r;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        // (a separate multiply and add: an fma of two scalar operands here miscompiles on
+        // gfx950, ROCm 7.2 — "VOP* instruction violates constant bus restriction")
+        float b = K * m_in[k] + Bb + (m_skip ? m_skip[k] : 0.0f);
+        r.pk |= range_exp(b * 1.001f) << (8 * k);    // margin for the fp32 rounding of the sums
+    }
+    r.pk = __builtin_amdgcn_readfirstlane(r.pk);
+    return r;
+}
+
+// activation reader for the heads (join of the two parts, times the board's scale 2^s)
 template <int F, int NPIX>
 struct ActH2 {
     const uint16_t* p;
+    int pk = 0;                                      // the image's RangeS exponents
+    __device__ float mul(int b) const { return pow2f((pk >> (8 * b)) & 0xFF); }
     __device__ void load8(int row, int k0, float (&v)[8]) const {
         typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
         const int o = CfgH<F, NPIX>::at(row, k0 / H2_K, (k0 % H2_K) >> 3);
@@ -218,42 +312,115 @@ __device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __rest
 }
 
 // v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
-// channels of one pixel per tile -> two 8-byte writes
-template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP>
+// channels of one pixel per tile -> two 8-byte writes.
+// Activation range (ActRange above), two modes. RANGED false (every pass first): the values are
+// stored unscaled, and a board with a value past f16's range sets its bit in the pass's overflow
+// word *ovw (LDS; a wave-uniform test, one compare per value as the sticky flag always cost).
+// RANGED true (only a pass whose word is set, re-run for those boards): the accumulator is
+// multiplied by 2^sin[b] and the stored value by 2^-sout[b] (the scaled branch, wave-uniform),
+// and the per-board max of the true outputs goes to rm_out[b][wave] (lane 0) for the next
+// layer's bound; a stored max past f16's range would be a bound error (the sticky word ovf).
+template <int F, int NPIX, int CTW, int PTW, bool RES, bool KEEP, class G>
 __device__ __forceinline__ void epilogue_h2(uint16_t* __restrict__ out,
                                             const f32x4 (&acc)[CTW][PTW], EpiH<CTW, PTW>& er,
-                                            const WaveTilesH<F, CTW, PTW>& wt, int lane,
-                                            bool& ovf) {
+                                            const WaveTilesH<F, CTW, PTW>& wt, int lane, int wave,
+                                            bool& ovf, bool rg, const RangeS<G::NBRD>& sin,
+                                            const RangeS<G::NBRD>& sout, float* rm_out,
+                                            unsigned* ovw) {
     using C = CfgH<F, NPIX>;
+    constexpr int NB = G::NBRD;
+    // LB: a lane's pixels all belong to one board (ILV: board = pixel column group; NB = 1), so
+    // one running max / overflow flag and one pair of multipliers per lane; else (packed 6x6)
+    // per board (max) or per tile (flag)
+    constexpr bool LB = G::ILVD || NB == 1;
+    constexpr int NM = LB ? 1 : NB;
+    constexpr int NO = LB ? 1 : PTW;
     typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    float mt[NM];                                    // max of this lane's outputs (ranged)
+    bool oflow[NO];                                  // a value past f16's range (not ranged)
 #pragma unroll
-    for (int c = 0; c < CTW; ++c)
+    for (int u = 0; u < NM; ++u) mt[u] = 0.0f;
 #pragma unroll
-        for (int u = 0; u < PTW; ++u) {
-            const int n0 = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
-            const int o = C::at(wt.px[u], n0 / H2_K, (n0 % H2_K) >> 3) + (n0 & 4);
-            u32x2 d0, d1;
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                f32x2 v;
-#pragma unroll
-                for (int e = 0; e < 2; ++e) {
-                    const int j = 2 * hf + e;
-                    float x = fmaf(acc[c][u][j], er.isc[c][j], er.bias[c][j]);
-                    if (RES) x += er.res[c][u][j];
-                    x = fmaxf(x, 0.0f);
-                    ovf |= x >= 65520.0f;
-                    if constexpr (KEEP) er.res[c][u][j] = x;
-                    v[e] = x;
-                }
-                uint32_t h0, h1;
-                split2x2(v, h0, h1);
-                d0[hf] = h0;
-                d1[hf] = h1;
-            }
-            *reinterpret_cast<u32x2*>(out + o) = d0;
-            *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
+    for (int u = 0; u < NO; ++u) oflow[u] = false;
+    auto body = [&](auto scaled, auto ranged) {
+        constexpr bool SC = decltype(scaled)::value, RANGED = decltype(ranged)::value;
+        float mi0 = 1.0f, mo0 = 1.0f;
+        if constexpr (SC && LB) {
+            mi0 = sin.mul(G::board_of(wt.px[0]), 1);
+            mo0 = sout.mul(G::board_of(wt.px[0]), -1);
         }
+#pragma unroll
+        for (int c = 0; c < CTW; ++c)
+#pragma unroll
+            for (int u = 0; u < PTW; ++u) {
+                const int n0 = (wt.ct0 + c) * H2_TM + 4 * (lane >> 4);
+                const int o = C::at(wt.px[u], n0 / H2_K, (n0 % H2_K) >> 3) + (n0 & 4);
+                float mi = mi0, mo = mo0;
+                if constexpr (SC && !LB) {
+                    mi = sin.mul(G::board_of(wt.px[u]), 1);
+                    mo = sout.mul(G::board_of(wt.px[u]), -1);
+                }
+                u32x2 d0, d1;
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    f32x2 v;
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int j = 2 * hf + e;
+                        float x = fmaf(SC ? acc[c][u][j] * mi : acc[c][u][j], er.isc[c][j],
+                                       er.bias[c][j]);
+                        if (RES) x += er.res[c][u][j];
+                        x = fmaxf(x, 0.0f);
+                        if constexpr (!RANGED) {
+                            oflow[LB ? 0 : u] |= x >= 65520.0f;
+                        } else if constexpr (LB) {
+                            mt[0] = fmaxf(mt[0], x);
+                        } else {
+                            const int bu = G::board_of(wt.px[u]);
+#pragma unroll
+                            for (int k = 0; k < NB; ++k) mt[k] = bu == k ? fmaxf(mt[k], x) : mt[k];
+                        }
+                        if constexpr (KEEP) er.res[c][u][j] = x;
+                        v[e] = SC ? x * mo : x;
+                    }
+                    uint32_t h0, h1;
+                    split2x2(v, h0, h1);
+                    d0[hf] = h0;
+                    d1[hf] = h1;
+                }
+                *reinterpret_cast<u32x2*>(out + o) = d0;
+                *reinterpret_cast<u32x2*>(out + C::PLANE + o) = d1;
+            }
+    };
+    if (!rg) {
+        body(std::false_type{}, std::false_type{});
+        bool any = false;
+#pragma unroll
+        for (int u = 0; u < NO; ++u) any |= oflow[u];
+        if (__builtin_amdgcn_ballot_w64(any) != 0ull) {      // rare: which boards
+            unsigned bits = 0;
+#pragma unroll
+            for (int u = 0; u < NO; ++u)
+#pragma unroll
+                for (int k = 0; k < NB; ++k)
+                    if (__builtin_amdgcn_ballot_w64(oflow[u] && G::board_of(wt.px[u]) == k))
+                        bits |= 1u << k;
+            if (lane == 0) atomicOr(ovw, bits);
+        }
+        return;
+    } else {
+        if (sin.any() || sout.any())
+            body(std::true_type{}, std::true_type{});
+        else
+            body(std::false_type{}, std::true_type{});
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            float m = LB ? (G::board_of(wt.px[0]) == k ? mt[0] : 0.0f) : mt[k];
+            m = wave_max_nonneg(m);
+            ovf |= m * pow2f(-sout.s(k)) >= 65520.0f;
+            if (lane == 0) rm_out[4 * k + wave] = m;
+        }
+    }
 }
 
 __device__ __forceinline__ f32x4 mfma_h(f16x8 a, f16x8 b, f32x4 c) {
@@ -298,7 +465,9 @@ __device__ __forceinline__ void stem_h2_load(const uint16_t* __restrict__ blob,
 template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV>
 __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__ out,
                                         const f16x8 (&w)[CTW][2], int wave, int lane,
-                                        EpiH<CTW, PTW>& er, bool& ovf) {
+                                        EpiH<CTW, PTW>& er, bool& ovf, bool rg,
+                                        const RangeS<NBOARD>& sout, float* rm_out,
+                                        unsigned* ovw) {
     const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
     // K order h2_stem_slot: this lane group's taps 2g, 2g + 1 and (groups 0, 1) part of tap 8
     const int kg = lane >> 4, ta = 2 * kg, tb = 2 * kg + 1;
@@ -346,8 +515,9 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 #endif
     }
     STEM_T(5);
-    epilogue_h2<F, GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>::NPIX, CTW, PTW, false, true>(
-        out, acc, er, wt, lane, ovf);
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
+    epilogue_h2<F, G::NPIX, CTW, PTW, false, true, G>(out, acc, er, wt, lane, wave, ovf, rg,
+                                                      RangeS<NBOARD>{}, sout, rm_out, ovw);
 }
 
 // The stem from the leaves' bitboards (the fused self-play kernel: select_phase leaves each
@@ -357,7 +527,10 @@ __device__ __forceinline__ void stem_h2(const float* xin, uint16_t* __restrict__
 template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV>
 __device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
                                              uint16_t* __restrict__ out, const f16x8 (&w)[CTW][2],
-                                             int wave, int lane, EpiH<CTW, PTW>& er, bool& ovf) {
+                                             int wave, int lane, EpiH<CTW, PTW>& er, bool& ovf,
+                                             bool rg,
+                                             const RangeS<NBOARD>& sout, float* rm_out,
+                                             unsigned* ovw) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
     const WaveTilesH<F, CTW, PTW> wt(wave, lane, ILV);
@@ -399,19 +572,23 @@ __device__ __forceinline__ void stem_h2_bits(const uint64_t (&pl)[NBOARD][3],
 #pragma unroll
         for (int u = 0; u < PTW; ++u) acc[c][u] = f32x4{};
     mma3<CTW, PTW, 0, 2>(acc, a, w);
-    epilogue_h2<F, G::NPIX, CTW, PTW, false, true>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, G::NPIX, CTW, PTW, false, true, G>(out, acc, er, wt, lane, wave, ovf, rg,
+                                                      RangeS<NBOARD>{}, sout, rm_out, ovw);
 }
 
-template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP = 0>
+template <int F, int NBOARD, int CTW, int PTW, bool RES, int BS, bool ILV, int GRP,
+          int PD = RVZ_H2_PD, int APD = RVZ_H2_APD>
 __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                         const H2W& wr, int wl,   // layer base, f16x8 units
                                         const float* __restrict__ bias,
                                         const float* __restrict__ isc, int wave, int lane,
-                                        f16x8 (&bc)[RVZ_H2_PD][CTW][2], EpiH<CTW, PTW>& er,
-                                        bool& ovf) {
+                                        f16x8 (&bc)[PD][CTW][2], EpiH<CTW, PTW>& er,
+                                        bool& ovf, bool rg, const RangeS<NBOARD>& sin,
+                                        const RangeS<NBOARD>& sout, float* rm_out,
+                                        unsigned* ovw) {
     using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
     using C = CfgH<F, G::NPIX>;
-    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT, PD = RVZ_H2_PD, APD = RVZ_H2_APD;
+    constexpr int KS = C::KS, CT = C::CT, NIT = C::NIT;
     // ILV: tile 0 is board row 0 (pixel group 0) or row 7 (group 1), and the taps with dr = -1
     // (row 0) or dr = +1 (row 7) leave the boards for all its pixels: tile 0's A loads and MFMAs
     // are skipped in those k-steps (1/12 of the conv MFMAs).
@@ -433,7 +610,14 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
     unsigned pmask[PTW];                              // valid taps in iteration order
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) pmask[u] = G::taps(wt.px[u]);
+    for (int u = 0; u < PTW; ++u) {
+        pmask[u] = G::taps(wt.px[u]);
+        // opaque per conv (NBOARD > 1): the per-tap, per-tile A addresses derive from it, and
+        // hoisted out of the residual loop they held 2 x 9 x PTW registers across the whole tower
+        // (k_play spilled them in the packed 6x6 geometry); one board per workgroup has the
+        // registers and forms them faster once
+        if constexpr (NBOARD > 1) asm volatile("" : "+v"(pmask[u]));
+    }
     f32x4 acc[CTW][PTW];
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
@@ -494,7 +678,8 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
 #pragma unroll
             for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
     // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
-    epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES>(out, acc, er, wt, lane, ovf);
+    epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES, G>(out, acc, er, wt, lane, wave, ovf, rg, sin, sout,
+                                                   rm_out, ovw);
 }
 
 // the leaf planes of NBOARD boards -> the halo-padded stem input xin[b][10x10][4] (halo and, for
@@ -524,6 +709,18 @@ struct XinStage {
 #pragma unroll
         for (int j = 0; j < PER; ++j)
             if (tid + j * NTHR < N) xin[tid + j * NTHR] = v[j];
+    }
+    // per board: the wave's max |input| -> rm[4 * b + wave] (RangeLds; the stem's bound)
+    __device__ void maxima(float* rm, int tid, int wave) const {
+#pragma unroll
+        for (int b = 0; b < NBOARD; ++b) {
+            float m = 0.0f;
+#pragma unroll
+            for (int j = 0; j < PER; ++j)
+                m = (tid + j * NTHR) / 400 == b ? fmaxf(m, fabsf(v[j])) : m;
+            m = wave_max_nonneg(m);
+            if ((tid & 63) == 0) rm[4 * b + wave] = m;
+        }
     }
 };
 
@@ -558,6 +755,149 @@ struct HeadsInLds {
         if (sl < nslots) in[sl * ROW + (i < PIN ? i : PK + (i - PIN))] = v;
     }
 };
+
+// The stem and the residual tower of one pass (h2_pass). RG (RANGED) false: every pass, values
+// stored unscaled, boards that overflowed set their bit in the pass's overflow words; RG true: a
+// re-run for those boards (mask) with the activation range scaled (ActRange), the others
+// unscaled as before, so every row's outputs still depend only on its own position. GR: the
+// ILV pixel group (conv_h2's tile-0 skip window). Returns the final image's scale exponents.
+template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV, int GR, bool RG>
+__device__ __forceinline__ RangeS<NBOARD> h2_trunk(char* smem, const float* __restrict__ x,
+                                                   const int (&gb)[NBOARD], const uint64_t* bits,
+                                                   const float* __restrict__ prm, const Layout& L,
+                                                   const uint16_t* __restrict__ blob,
+                                                   int n_blocks, int tid, int lane, int wave,
+                                                   bool& ovf, unsigned mask) {
+    const BarWG bar{};
+    using WT = WaveTilesH<F, CTW, PTW>;
+    using G = GeoH<NBOARD, BS, 64 * CTW * H2_TM / F, ILV>;
+    using C = CfgH<F, G::NPIX>;
+    constexpr int NTHR = 256;
+    uint16_t* actA = reinterpret_cast<uint16_t*>(smem);
+    uint16_t* actB = actA + C::ACT;
+    float* xin = reinterpret_cast<float*>(actB);     // free until the first conv writes B
+    const H2W wr(blob, h2_blob_elems(F, n_blocks));
+    const RangeLds rl{reinterpret_cast<float*>(smem + C::RMAX)};
+    constexpr int PD = RG ? 1 : RVZ_H2_PD, APD = RG ? 0 : RVZ_H2_APD;
+    PASS_NOW(tp0);
+    f16x8 bc[PD][CTW][2];
+    if (n_blocks > 0) {
+        const int wu = WT(wave, lane).ct0 * 64;
+#pragma unroll
+        for (int s = 0; s < PD; ++s) {
+            const int f = wu + h2_frag<F>(s);
+#pragma unroll
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) bc[s][c][p] = wr.load(f + (p * C::CT + c) * 64, lane);
+        }
+    }
+    EpiH<CTW, PTW> er;
+    f16x8 ws[CTW][2];
+    // RANGED: {K, Bb} per layer from the blob's range table; the per-wave maxima in LDS
+    // (RangeLds: slots 0 / 2 the inputs of even / odd blocks, 1 conv A's outputs); the
+    // exponents of boards outside the mask forced to 0
+    const float* rng = reinterpret_cast<const float*>(blob + h2_range_off(F, n_blocks));
+    unsigned keep = 0;                            // 0xFF per masked board
+#pragma unroll
+    for (int k = 0; k < NBOARD; ++k) keep |= (mask >> k & 1u) ? 0xFFu << (8 * k) : 0u;
+    auto masked = [&](RangeS<NBOARD> r) {
+        r.pk &= (int)keep;
+        return r;
+    };
+    auto bound = [&](const float (&m)[NBOARD], int l, const float* m_skip) {
+        return RG ? masked(range_out(m, rng[2 * l], rng[2 * l + 1], m_skip)) : RangeS<NBOARD>{};
+    };
+    RangeS<NBOARD> simg;                          // the stored image's scale exponents
+    float m_in[NBOARD];                           // (the stem's input maxima)
+    if (bits) {   // leaf bitboards in LDS: no global round trip, no padded image
+        uint64_t pl[NBOARD][3];
+#pragma unroll
+        for (int b = 0; b < NBOARD; ++b)
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                const uint64_t v = bits[3 * b + ch];
+                pl[b][ch] = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+            }
+        stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+#pragma unroll
+        for (int k = 0; k < NBOARD; ++k) m_in[k] = 1.0f;      // 0 / 1 planes
+        simg = bound(m_in, 0, nullptr);
+        stem_h2_bits<F, NBOARD, CTW, PTW, BS, ILV>(pl, actA, ws, wave, lane, er, ovf, RG, simg,
+                                                       rl.slot(0), rl.ovw(wave));
+    } else {
+        XinStage<NBOARD, BS, NTHR> st;
+        st.load(x, gb, tid);
+        stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
+        STEM_T(0);
+        st.store(xin, tid);
+        if constexpr (RG) st.maxima(rl.slot(1), tid, wave);
+        STEM_T(1);
+        bar();
+        STEM_T(2);
+        if constexpr (RG) {
+#pragma unroll
+            for (int k = 0; k < NBOARD; ++k) m_in[k] = rl.read(1, k);
+            simg = bound(m_in, 0, nullptr);
+        }
+        stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf, RG, simg,
+                                                  rl.slot(0), rl.ovw(wave));
+        STEM_T(3);
+    }
+    bar();
+    PHASE(1);
+    {
+        PASS_NOW(tp1);
+        PASS_ADD(0, tp1 - tp0);
+    }
+    const int64_t LW = h2_layer_elems(F);
+    const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
+    for (int blk = 0; blk < n_blocks; ++blk) {
+        const int l1 = 2 * blk, l2 = 2 * blk + 1, sb = 2 * (blk & 1);
+        // conv A's output scale from the block input's maxima (slot sb; recomputed for conv B,
+        // so nothing but the packed exponents lives across a conv)
+        auto scale_t = [&] {
+            float m[NBOARD];
+#pragma unroll
+            for (int k = 0; k < NBOARD; ++k) m[k] = RG ? rl.read(sb, k) : 0.0f;
+            return bound(m, 1 + l1, nullptr);
+        };
+        conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR, PD, APD>(
+            actA, actB, wr, (int)(l1 * LW / 8), prm + L.res_b + (size_t)l1 * F, isc + l1 * F,
+            wave, lane, bc, er, ovf, RG, simg, scale_t(), rl.slot(1), rl.ovw(wave));
+        if (blk == 0) PHASE(5);
+        bar();
+        if (blk == 0) PHASE(6);
+        {
+            float m_t[NBOARD], m_blk[NBOARD];
+#pragma unroll
+            for (int k = 0; k < NBOARD; ++k) {
+                m_t[k] = RG ? rl.read(1, k) : 0.0f;
+                m_blk[k] = RG ? rl.read(sb, k) : 0.0f;                // the skip input
+            }
+            const RangeS<NBOARD> st = scale_t();
+            simg = bound(m_t, 1 + l2, m_blk);
+            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR, PD, APD>(
+                actB, actA, wr, (int)(l2 * LW / 8), prm + L.res_b + (size_t)l2 * F,
+                isc + l2 * F, wave, lane, bc, er, ovf, RG, st, simg, rl.slot(2 - sb),
+                rl.ovw(wave));
+        }
+        bar();
+    }
+    return simg;
+}
+
+// The ranged re-run as a call: inlined next to the unscaled copy its registers pushed the hot
+// path into spills; as a function the spills and the call's saves run only on the rare path.
+template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV, int GR>
+__device__ __attribute__((noinline)) RangeS<NBOARD> h2_trunk_ranged(
+    char* smem, const float* __restrict__ x, const int (&gb)[NBOARD], const uint64_t* bits,
+    const float* __restrict__ prm, const Layout& L, const uint16_t* __restrict__ blob,
+    int n_blocks, int tid, int lane, int wave, bool& ovf, unsigned mask) {
+    return h2_trunk<F, NBOARD, CTW, PTW, BS, ILV, GR, true>(smem, x, gb, bits, prm, L, blob,
+                                                            n_blocks, tid, lane, wave, ovf, mask);
+}
 
 // One pass of the workgroup (256 threads) over NBOARD boards: board b's leaf planes are row gb[b]
 // of x ([rows][3][BS*BS], gb[b] < 0: no board), its 1x1 head-conv outputs go to row gb[b] of
@@ -598,79 +938,33 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     // from the weight prefetch to the last residual block: ILV, one instance per pixel group
     // (its own tile-0 skip window, conv_h2), chosen by a wave-uniform branch
     const bool grp1 = ILV && wave / WT::CG != 0;
-    auto trunk = [&](auto grp) {
-        constexpr int GR = decltype(grp)::value;
-        f16x8 bc[RVZ_H2_PD][CTW][2];
-        if (n_blocks > 0) {
-            const int wu = WT(wave, lane).ct0 * 64;
-#pragma unroll
-            for (int s = 0; s < RVZ_H2_PD; ++s) {
-                const int f = wu + h2_frag<F>(s);
-#pragma unroll
-                for (int c = 0; c < CTW; ++c)
-#pragma unroll
-                    for (int p = 0; p < 2; ++p) bc[s][c][p] = wr.load(f + (p * C::CT + c) * 64, lane);
-            }
-        }
-        EpiH<CTW, PTW> er;
-        f16x8 ws[CTW][2];
-        if (bits) {   // leaf bitboards in LDS: no global round trip, no padded image
-            uint64_t pl[NBOARD][3];
-#pragma unroll
-            for (int b = 0; b < NBOARD; ++b)
-#pragma unroll
-                for (int ch = 0; ch < 3; ++ch) {
-                    const uint64_t v = bits[3 * b + ch];
-                    pl[b][ch] = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-                                (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-                }
-            stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
-            stem_h2_bits<F, NBOARD, CTW, PTW, BS, ILV>(pl, actA, ws, wave, lane, er, ovf);
-        } else {
-            XinStage<NBOARD, BS, NTHR> st;
-            st.load(x, gb, tid);
-            stem_h2_load<F, NBOARD, CTW, PTW>(blob, prm, L, n_blocks, wave, lane, er, ws);
-            STEM_T(0);
-            st.store(xin, tid);
-            STEM_T(1);
-            bar();
-            STEM_T(2);
-            stem_h2<F, NBOARD, CTW, PTW, BS, ILV>(xin, actA, ws, wave, lane, er, ovf);
-            STEM_T(3);
-        }
-        bar();
-        PHASE(1);
-        {
-            PASS_NOW(tp1);
-            PASS_ADD(0, tp1 - tp0);
-        }
-        const int64_t LW = h2_layer_elems(F);
-        const float* isc = reinterpret_cast<const float*>(blob + h2_scale_off(F, n_blocks)) + F;
-        for (int blk = 0; blk < n_blocks; ++blk) {
-            const int l1 = 2 * blk, l2 = 2 * blk + 1;
-            conv_h2<F, NBOARD, CTW, PTW, false, BS, ILV, GR>(actA, actB, wr, (int)(l1 * LW / 8),
-                                                             prm + L.res_b + (size_t)l1 * F,
-                                                             isc + l1 * F, wave, lane, bc, er, ovf);
-            if (blk == 0) PHASE(5);
-            bar();
-            if (blk == 0) PHASE(6);
-            conv_h2<F, NBOARD, CTW, PTW, true, BS, ILV, GR>(actB, actA, wr, (int)(l2 * LW / 8),
-                                                            prm + L.res_b + (size_t)l2 * F,
-                                                            isc + l2 * F, wave, lane, bc, er, ovf);
-            bar();
-        }
-    };
-    if (grp1)
-        trunk(std::integral_constant<int, 1>{});
-    else
-        trunk(std::integral_constant<int, 0>{});
+    const RangeLds rl{reinterpret_cast<float*>(smem + C::RMAX)};
+    if (lane == 0) *rl.ovw(wave) = 0u;                // this wave's overflow word (its epilogues)
+    // the stem and the residual tower. RANGED false: every pass, values stored unscaled, boards
+    // that overflowed set their bit in the pass's overflow word; RANGED true: a re-run for those
+    // boards (mask) with the activation range scaled (ActRange), the others unscaled as before,
+    // so every row's outputs still depend only on its own position
+    RangeS<NBOARD> simg =
+        grp1 ? h2_trunk<F, NBOARD, CTW, PTW, BS, ILV, 1, false>(smem, x, gb, bits, prm, L, blob,
+                                                                 n_blocks, tid, lane, wave, ovf, 0u)
+             : h2_trunk<F, NBOARD, CTW, PTW, BS, ILV, 0, false>(smem, x, gb, bits, prm, L, blob,
+                                                                 n_blocks, tid, lane, wave, ovf, 0u);
+    // the overflow words are final after the tower's last barrier (n_blocks = 0: the stem's)
+    const unsigned omask = rl.ov_all();
+    if (omask != 0u) {                                // rare: re-run the boards that overflowed
+        __syncthreads();                              // every wave has read the words
+        simg = grp1 ? h2_trunk_ranged<F, NBOARD, CTW, PTW, BS, ILV, 1>(
+                          smem, x, gb, bits, prm, L, blob, n_blocks, tid, lane, wave, ovf, omask)
+                    : h2_trunk_ranged<F, NBOARD, CTW, PTW, BS, ILV, 0>(
+                          smem, x, gb, bits, prm, L, blob, n_blocks, tid, lane, wave, ovf, omask);
+    }
     PHASE(2);
     PASS_NOW(tp2);
     PASS_ADD(1, tp2 - tp0);   // stem + tower
     // the 1x1 head convs -> work (the FC heads are the next launch, k_heads_mfma)
-    head_convs<F, NBOARD, NTHR, BS, true, ILV>(ActH2<F, G::NPIX>{actA},
-                                              reinterpret_cast<float*>(actB), prm, L, hout, tid,
-                                              bar);
+    const ActH2<F, G::NPIX> act{actA, simg.pk};
+    head_convs<F, NBOARD, NTHR, BS, true, ILV>(act, reinterpret_cast<float*>(actB), prm, L, hout,
+                                              tid, bar);
 #ifdef RVZ_PLAY_TIMING
     {
         PASS_NOW(tp3);

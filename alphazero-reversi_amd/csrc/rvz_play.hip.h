@@ -308,8 +308,9 @@ void k_play(PlayCtx ctx0) {
         task_plies = queue ? 1 : c.a.plies;
     }
     bool ovf = false;
-    int n_rows = 0;                      // rows this workgroup evaluated
-    unsigned n_hits = 0, n_ins = 0;      // table hits (per wave) / inserts
+    // the workgroup's rows, table hits and inserts, in LDS (no registers held across the phases)
+    __shared__ unsigned s_cnt[3];
+    if (tid < 3) s_cnt[tid] = 0u;
     if (tid == 0) {
         const PlayArgs& a = play_ctx().a;
         s_tgen = a.tab ? __hip_atomic_load(a.tgen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
@@ -441,7 +442,7 @@ void k_play(PlayCtx ctx0) {
                                     // back in this wave
                                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
                                     f |= PF_READY;
-                                    ++n_hits;
+                                    if (lane == 0) atomicAdd(&s_cnt[1], 1u);
                                     continue;
                                 }
                             }
@@ -533,7 +534,7 @@ void k_play(PlayCtx ctx0) {
             __syncthreads();
             const int nq = __builtin_amdgcn_readfirstlane(s_nq);
             if (nq == 0) break;   // every game has committed its plies
-            n_rows += nq;
+            if (tid == 0) s_cnt[0] += (unsigned)nq;
             PT_NOW(t_c2);
 
             // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
@@ -576,7 +577,9 @@ void k_play(PlayCtx ctx0) {
                     const PlayArgs& a = play_ctx().a;
                     const uint64_t P = q_bits[3 * i], O = q_bits[3 * i + 1], Vb = q_bits[3 * i + 2];
                     if (__popcll(P | O) <= a.tmaxd)
-                        n_ins += tab_insert<BS>(a, s_tgen, P, O, Vb, opaque_tid() & 63, q_rows[i]);
+                        if (tab_insert<BS>(a, s_tgen, P, O, Vb, opaque_tid() & 63, q_rows[i]) &&
+                            (opaque_tid() & 63) == 0)
+                            atomicAdd(&s_cnt[2], 1u);
                 }
             }
             for (int j = tid; j < ng; j += 256)
@@ -611,10 +614,11 @@ void k_play(PlayCtx ctx0) {
     float* ovw = play_ctx().a.ovf;
     if (ovf && ovw) *ovw = 1.0f;   // benign race: every writer stores 1
     unsigned long long* rows = play_ctx().a.rows;
-    if (rows && tid == 0) atomicAdd(rows, (unsigned long long)n_rows);
+    __syncthreads();                       // every wave's counts are in
+    if (rows && tid == 0) atomicAdd(rows, (unsigned long long)s_cnt[0]);
     unsigned long long* ts = play_ctx().a.tstats;
-    if (ts && (tid & 63) == 0) {   // per wave: its hits and inserts
-        if (n_hits) atomicAdd(ts, (unsigned long long)n_hits);
-        if (n_ins) atomicAdd(ts + 1, (unsigned long long)n_ins);
+    if (ts && tid == 0) {          // the workgroup's hits and inserts
+        if (s_cnt[1]) atomicAdd(ts, (unsigned long long)s_cnt[1]);
+        if (s_cnt[2]) atomicAdd(ts + 1, (unsigned long long)s_cnt[2]);
     }
 }

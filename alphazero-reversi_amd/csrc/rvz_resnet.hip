@@ -116,10 +116,23 @@ __global__ __launch_bounds__(64) void k_h2_weights(const float* __restrict__ prm
         const int t = i / F, k = i % F;
         return prm[L.res_w + (((int64_t)lyr * 9 + t) * F + n) * F + k];
     };
-    float m = 0.0f;
-    for (int i = lane; i < cnt; i += 64) m = fmaxf(m, fabsf(wget(i)));
+    float m = 0.0f, l1 = 0.0f;
+    for (int i = lane; i < cnt; i += 64) {
+        m = fmaxf(m, fabsf(wget(i)));
+        l1 += fabsf(wget(i));
+    }
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    for (int o = 32; o >= 1; o >>= 1) {
+        m = fmaxf(m, __shfl_xor(m, o));
+        l1 += __shfl_xor(l1, o);
+    }
+    if (lane == 0) {   // the activation-range table: max over channels (non-negative floats
+                       // order as their bit patterns: an unsigned max, zeroed by the host first)
+        unsigned* rng = reinterpret_cast<unsigned*>(blob + h2_range_off(F, NB)) + 2 * (lyr + 1);
+        const float b = lyr < 0 ? prm[L.stem_b + n] : prm[L.res_b + (int64_t)lyr * F + n];
+        atomicMax(rng, __float_as_uint(l1));
+        atomicMax(rng + 1, __float_as_uint(fabsf(b)));
+    }
     int e = 0;
     if (m > 0.0f) {
         frexpf(m, &e);                         // m = f * 2^e, f in [0.5, 1): floor(log2 m) = e - 1
@@ -285,6 +298,11 @@ int rvz_resnet_h2_weights(const float* params, int32_t filters, int32_t blocks, 
     // the prefetch padding after the last layer reads zeros
     if (hipMemsetAsync(blob + 2 * blocks * h2_layer_elems(filters), 0,
                        h2_pad_ksteps(filters) * h2_kstep_elems(filters) * 2, s) != hipSuccess)
+        return RVZ_EHIP;
+    // the activation-range table is a max over the launch's workgroups: zeroed first
+    if (hipMemsetAsync(blob + h2_range_off(filters, blocks), 0,
+                       (h2_blob_elems(filters, blocks) - h2_range_off(filters, blocks)) * 2,
+                       s) != hipSuccess)
         return RVZ_EHIP;
     hipLaunchKernelGGL(k_h2_weights, dim3(filters, 1 + 2 * blocks), dim3(64), 0, s, params, L,
                        (int)filters, (int)blocks, blob);

@@ -85,8 +85,10 @@ __device__ __forceinline__ void head_convs(const Act& act, float* part,
             if (!on) break;
             float v[8];
             act.load8(arow, cg * CPG + 8 * k8, v);
+            const float mb = act.mul(b);              // the board's activation scale (1: none)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
+                v[j] *= mb;
                 p0 = fmaf(v[j], w0[8 * k8 + j], p0);
                 p1 = fmaf(v[j], w1[8 * k8 + j], p1);
                 p2 = fmaf(v[j], w2[8 * k8 + j], p2);

@@ -386,13 +386,15 @@ class Engine:
 
         fused_softmax=False applies torch's F.softmax (the reference's mcts.py:596) before the
         expand kernel instead of the kernel's fused softmax. skip_last_eval=True does not
-        evaluate the last batch (rvz_search_skip; bit-identical visits, one NN call fewer)."""
+        evaluate the last batch (rvz_search_skip; bit-identical visits, one NN call fewer) when
+        a search has two batches or more: a single batch's leaf is the root, which the act needs
+        expanded, so it is evaluated."""
         self._bind(evaluator)
         self.search_begin()
         k = 0
         while self.search_step():
             k += 1
-            if skip_last_eval and k == self.n_batches:
+            if skip_last_eval and k == self.n_batches > 1:
                 self.search_skip()
                 break
             if self.compact_leaves and getattr(evaluator, "accepts_live_count", False):

@@ -590,21 +590,28 @@ def cpu_baseline(args, net):
 
 def stored_traffic(args, kernel, plies=None):
     """HBM bytes per launch of `kernel` from the committed PMC passes (--pmc), quoted only for the
-    configuration they were measured on (C2, 4,096 games), with their source named. k_play: the
-    passes' launches cover `plies_per_launch` plies; a launch of another length gets the bytes
-    scaled by its plies, and the label says so."""
-    if not (os.path.exists(args.pmc) and args.config == "c2" and args.games == 4096):
+    configuration they were measured on, with their source named. k_play: key "play" (C2's
+    launches) or "play_<config>" (tools/pmc_play_traffic.py: C3, C5), each with its games per
+    GPU and plies per launch; a launch of another length gets the bytes scaled by its plies, and
+    the label says so. The search kernels' entries were measured at C2 (4,096 games)."""
+    if not os.path.exists(args.pmc):
         return None, None
     try:
         pmc = json.load(open(args.pmc))
     except Exception:
         return None, None
-    b = pmc.get(kernel, {}).get("hbm_bytes_per_launch")
+    key = f"play_{args.config}" if kernel == "play" and args.config != "c2" else kernel
+    ent = pmc.get(key, {})
+    games = ent.get("games", 4096)
+    if ent.get("config", "c2") != args.config or games != args.games:
+        return None, None
+    b = ent.get("hbm_bytes_per_launch")
     if b is None:
         return None, None
-    src = (f"{os.path.relpath(args.pmc, ROOT)} ({pmc.get('source', 'stored rocprofv3 PMC passes')}"
+    src = (f"{os.path.relpath(args.pmc, ROOT)}[{key}] "
+           f"({ent.get('source') or pmc.get('source', 'stored rocprofv3 PMC passes')}"
            "; not measured in this run)")
-    pl = pmc.get(kernel, {}).get("plies_per_launch")
+    pl = ent.get("plies_per_launch")
     if plies and pl and plies != pl:
         b = round(b * plies / pl)
         src += f"; scaled from {pl}-ply to {plies}-ply launches"
@@ -797,9 +804,8 @@ def selfplay(args, device, rank, world, full=True):
     ach = fpr * rows_tr / (t_tr * 1e-3) / 1e12
     ach_u = upr * rows_tr / (t_tr * 1e-3) / 1e12
     region = fpr * rows / (t1 - t0) / 1e12      # every lane's evaluated rows / timed wall time
-    traffic, traffic_src = (stored_traffic(args, "play" if args.fused else "nn_trunk",
-                                           ppg if args.fused else None)
-                            if full else (None, None))
+    traffic, traffic_src = (stored_traffic(args, "play", ppg) if args.fused else
+                            stored_traffic(args, "nn_trunk") if full else (None, None))
     roof = {"kernel": "k_play" if args.fused else ev.trunk_kernel_name, "bound": "mfma",
             "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4),

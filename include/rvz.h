@@ -122,6 +122,9 @@ int rvz_search_submit(rvz_engine *e, const float *policy, int32_t is_logits, con
  * discarded tree never reads (the leaf's children priors, W along the path; mcts.py:600-640), so
  * rvz_search_visits / rvz_act then back up the visit counts alone and return exactly the visits,
  * p and move of the evaluated search (tests/test_gpu_search.py::test_skip_last_eval_bit_exact).
+ * Needs a search of at least two batches (num_simulations > batch_size; RVZ_EINVAL otherwise:
+ * a single batch's leaf is the root, whose expansion the act needs; rvz_play's skip_last_eval
+ * is ignored for such searches).
  * Off unless called (one NN call fewer per move; not the reference's call sequence). bench.py's
  * headline uses it by default (--evals table, and --evals lazy: the memo + this, so the skipped
  * evaluation is made later only if a search reaches that position; rvz_play's skip_last_eval is

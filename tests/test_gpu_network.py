@@ -185,20 +185,86 @@ def test_evaluator_matches_reference_outputs(kernel):
     assert (p.argmax(1) == probs.argmax(1)).mean() > 0.99
 
 
-def test_h2_overflow_flag():
-    """h2 keeps activations as two f16 parts: an activation >= 65520 cannot be represented. The
-    kernel raises the sticky overflow word instead of returning silently wrong outputs."""
+def _fp64_outputs(net, x):
+    """The reference module's forward in fp64 on the CPU (ground truth for the range tests)."""
+    import copy
+    m = copy.deepcopy(net).double().cpu().eval()
+    with torch.no_grad():
+        lo, v = m(x.double().cpu())
+    return lo, v.reshape(-1)
+
+
+def _fp32_module_err(net, x, l64, v64):
+    with torch.no_grad():
+        lo, v = net(x)
+    return ((lo.double().cpu() - l64).abs().max().item(),
+            (v.reshape(-1).double().cpu() - v64).abs().max().item())
+
+
+@pytest.mark.parametrize("where", ["stem_bias", "tower_weights"])
+def test_h2_activation_range_is_scaled_not_overflowed(where):
+    """h2 keeps activations as two f16 parts, which overflow at 65520. Each
+    board's activation image is stored scaled by a power of two chosen from a bound on the
+    layer's outputs (ActRange, csrc/rvz_h2.hip.h), so a net whose activations reach ~1e5-1e7
+    evaluates fp32-class instead of raising: the stem bias at 1e5 (round 4's overflow case), or
+    the tower's conv weights scaled up so that activations grow block after block."""
     import rvz
     net = _bn_net(2, 64, seed=6)
-    x = (torch.rand(64, 3, 8, 8, device="cuda") > 0.6).float()
-    ev = rvz.LeafEvaluator(net, kernel="h2")
-    ev(x)
-    assert not ev.overflowed()
+    x = (torch.rand(256, 3, 8, 8, device="cuda") > 0.6).float()
     with torch.no_grad():
-        net.bn.bias.fill_(1e5)            # stem output ~1e5 > the f16 range
+        if where == "stem_bias":
+            net.bn.bias.fill_(1e5)            # stem output ~1e5 > the f16 range
+        else:
+            for blk in net.res_blocks:
+                blk.conv1.weight.mul_(12.0)
+                blk.conv2.weight.mul_(12.0)
+    l64, v64 = _fp64_outputs(net, x)
     ev = rvz.LeafEvaluator(net, kernel="h2")
-    ev(x)
-    assert ev.overflowed()
+    lo, v = ev(x)
+    assert not ev.overflowed()
+    scale = l64.abs().max().item()
+    assert scale > 1e4                        # the activations are past f16's range
+    e32, ev32 = _fp32_module_err(net, x, l64, v64)
+    err = (lo.double().cpu() - l64).abs().max().item()
+    verr = (v.double().cpu() - v64).abs().max().item()
+    assert err <= 4 * e32 + 1e-6 * scale, (err, e32, scale)
+    assert verr <= 4 * ev32 + 1e-6, (verr, ev32)
+
+
+def test_h2_activation_range_leaves_ordinary_nets_bitwise():
+    """The range table's bounds stay below 2^15 for ordinary nets, so nothing is scaled: the
+    outputs are those of the unscaled arithmetic, which the fixture and fp32-class tests pin;
+    here: the blob's range table holds K = max over channels of sum |w| and Bb = max |bias| of
+    every layer (BN folded), and a row's outputs do not depend on its pass partner."""
+    import rvz
+    from rvz.network import pack_resnet_params  # noqa: F401
+    net = _bn_net(2, 64, seed=3)
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    blob = ev.wsplit.cpu().numpy().view(np.uint16)
+    F, NB = 64, 2
+    n_el = blob.size
+    nl = 1 + 2 * NB
+    rng = blob[n_el - ((4 * nl + 7) // 8 * 8):][:4 * nl].view(np.float32).reshape(nl, 2)
+    folded = []
+    with torch.no_grad():
+        def fold(conv, bn):
+            s = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+            w = conv.weight * s.view(-1, 1, 1, 1)
+            b = bn.bias - bn.running_mean * s + (conv.bias * s if conv.bias is not None else 0)
+            return w.double().cpu(), b.double().cpu()
+        folded.append(fold(net.conv, net.bn))
+        for blk in net.res_blocks:
+            folded.append(fold(blk.conv1, blk.bn1))
+            folded.append(fold(blk.conv2, blk.bn2))
+    for i, (w, b) in enumerate(folded):
+        k = w.abs().reshape(w.shape[0], -1).sum(1).max().item()
+        assert abs(rng[i, 0] - k) <= 1e-5 * k, (i, rng[i], k)
+        assert abs(rng[i, 1] - b.abs().max().item()) <= 1e-6 * max(1.0, b.abs().max().item())
+    assert rng[:, 0].max() * 2 + rng[:, 1].max() < 2 ** 15
+    x = (torch.rand(64, 3, 8, 8, device="cuda") > 0.6).float()
+    lo, v = (t.clone() for t in ev(x))             # (the evaluator reuses its output buffers)
+    lo2, v2 = ev(x.flip(0).contiguous())
+    assert torch.equal(lo, lo2.flip(0)) and torch.equal(v, v2.flip(0))
 
 
 def test_h2_weight_blob():

@@ -231,10 +231,14 @@ def test_h2_fp32_class_on_trained_weights(tmp_path):
     assert verr["h2"] <= 4 * fp32v + 1e-7, verr
 
 
-def test_overflowing_evaluator_raises_in_selfplay(tmp_path):
-    """A net whose stem activations exceed the f16 range (|x| >= 65520): the h2 evaluator's
-    sticky overflow word makes SelfPlay / the runners' check raise RvzError instead of writing
-    records from invalid priors and values."""
+def test_large_activation_net_plays_in_selfplay(tmp_path):
+    """Round 4 raised here: a net whose stem activations exceed the f16 range (|x| >= 65520)
+    set h2's sticky overflow word and SelfPlay stopped. With the activation range scaled per
+    board the same net plays: SelfPlay and a graph-captured runner finish,
+    the overflow word stays clear, and the evaluator's outputs on the positions played are
+    fp32-class against the fp64 module. (A non-finite NN output still stops the tree: next
+    test.)"""
+    import copy
     import rvz
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
@@ -242,9 +246,8 @@ def test_overflowing_evaluator_raises_in_selfplay(tmp_path):
         net.bn.bias.fill_(1e5)
     sp = rvz.SelfPlay(net, {"num_simulations": 128, "seed": 1, "save_dir": str(tmp_path)})
     assert sp.evaluator.kernel == "h2"
-    with pytest.raises(rvz.RvzError):
-        sp.generate_games(4)
-    # the same through a graph-captured runner: the error surfaces at check()
+    games = sp.generate_games(4)
+    assert len(games) == 4 and not sp.evaluator.overflowed()
     eng = rvz.Engine(64, 128, 64)
     ev = rvz.LeafEvaluator(net, kernel="h2")
     run = rvz.SelfPlayRunner(eng, ev, autoreset=True)
@@ -252,8 +255,66 @@ def test_overflowing_evaluator_raises_in_selfplay(tmp_path):
     run.ply()
     run.capture()
     run.ply()
-    with pytest.raises(rvz.RvzError):
+    run.check()
+    assert not ev.overflowed()
+    x = torch.from_numpy(np.stack([s for g in games for s in g["states"]])).float().cuda()
+    m64 = copy.deepcopy(net).double().cpu().eval()
+    with torch.no_grad():
+        l64, v64 = m64(x.double().cpu())
+        l32, v32 = net(x)
+    lo, v = ev(x)
+    scale = l64.abs().max().item()
+    e32 = (l32.double().cpu() - l64).abs().max().item()
+    assert (lo.double().cpu() - l64).abs().max().item() <= 4 * e32 + 1e-6 * scale
+    assert (v.double().cpu() - v64.reshape(-1)).abs().max().item() <= \
+        4 * (v32.double().cpu() - v64).abs().max().item() + 1e-6
+
+
+def test_aggressive_training_never_overflows():
+    """the C4 loop's weights change every iteration; five SelfPlayTrainer
+    iterations at an aggressive learning rate (the activations grow) never raise and never set
+    the overflow word."""
+    from rvz.pipeline import SelfPlayTrainer
+    import rvz  # noqa: F401
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 2, 64).cuda()
+    spt = SelfPlayTrainer(net, 64, num_simulations=128, seed=3, train_steps=30, train_batch=64,
+                          lr=0.05)
+    for _ in range(5):
+        r = spt.run_iteration()
+        spt.runner.check()
+        assert not spt.evaluator.overflowed()
+        assert all(torch.isfinite(p).all() for p in net.parameters())
+    assert r["board_steps"] > 0
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_one_batch_searches_are_evaluated(fused):
+    """Regression (round 5): with num_simulations <= batch_size a search is one batch, whose
+    leaf is the root; the deferred last batch (skip_last_eval) left the root unexpanded, so the
+    act found no visited child and the games stalled (SelfPlayTrainer: "a game is not over after
+    60 plies"). The single batch is now evaluated: the same games as without skip_last_eval."""
+    import rvz
+    torch.manual_seed(0)
+    net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
+    moves = []
+    for skip in (True, False):
+        eng = rvz.Engine(48, 64, 64, memo=True, compact_leaves=True)
+        run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=5,
+                                 skip_last_eval=skip, fused=fused)
+        run.start()
+        ms = []
+        for _ in range(6):
+            run.ply()
+            ms.append(eng.idx_buf.clone())
         run.check()
+        assert int(run._plies.sum()) == 6 * 48
+        moves.append(torch.stack(ms))
+    assert torch.equal(moves[0], moves[1])
+    with pytest.raises(rvz.RvzError, match="two batches"):
+        eng.search_begin()
+        eng.search_step()
+        eng.search_skip()
 
 
 def test_non_finite_nn_output_sets_the_device_error_word():

@@ -124,15 +124,15 @@ def test_table_blob_switch_is_refused_inside_a_capture():
     every replay, so rvz_play refuses it there. After one eager play with the new evaluator the
     capture goes through, and its replays keep the table (hits accumulate)."""
     import rvz
-    G, S = 64, 96
+    G, S = 4096, 128                  # openings: the same positions in many games (hits)
     eng = rvz.Engine(G, S, 64, memo=True)
-    eng.table(1 << 12, 14)
+    eng.table(1 << 16, 14)
     ev_a = rvz.LeafEvaluator(_net(8, 1, 64, seed=1))
     ev_b = rvz.LeafEvaluator(_net(8, 1, 64, seed=2))
     run = rvz.SelfPlayRunner(eng, ev_a, autoreset=True, seed_base=3, skip_last_eval=True,
                              fused=True)
     run.start()
-    run._body(2)                      # the table's generation belongs to ev_a's blob
+    run._body(1)                      # the table's generation belongs to ev_a's blob
     eng.play_buffers(ev_b)
     run.evaluator = ev_b
     g = torch.cuda.CUDAGraph()
@@ -142,11 +142,12 @@ def test_table_blob_switch_is_refused_inside_a_capture():
     torch.cuda.synchronize()
     run._body(1)                      # eager: the generation moves to ev_b's blob
     run.capture(plies=1)
-    h0 = int(eng.table_stats[0].item())
+    h0, p0 = int(eng.table_stats[0].item()), int(run._plies.sum())
     for _ in range(3):
         run.ply()
     torch.cuda.synchronize()
     eng.check()
+    assert int(run._plies.sum()) - p0 == 3 * G
     assert int(eng.table_stats[0].item()) > h0
 
 

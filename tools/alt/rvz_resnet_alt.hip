@@ -75,6 +75,7 @@ struct ActF32 {
     int cs;
     __device__ void store(int row, int n, float v) const { p[row * cs + n] = v; }
     __device__ float load(int row, int k) const { return p[row * cs + k]; }
+    __device__ float mul(int) const { return 1.0f; }   // head_convs' per-board scale: none
     __device__ void load8(int row, int k0, float (&v)[8]) const {
         const f32x4 a = *reinterpret_cast<const f32x4*>(p + row * cs + k0);
         const f32x4 b = *reinterpret_cast<const f32x4*>(p + row * cs + k0 + 4);
@@ -98,6 +99,7 @@ struct ActSplit {
         const uint16_t* o = p + row * cs + k;
         return join3(o[0], o[plane], o[2 * plane]);
     }
+    __device__ float mul(int) const { return 1.0f; }   // head_convs' per-board scale: none
     __device__ void load8(int row, int k0, float (&v)[8]) const {
         typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
         const uint16_t* o = p + row * cs + k0;

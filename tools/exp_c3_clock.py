@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """C3's 10x128 evaluator two ways, for rocprofv3 --pmc passes (clock, MFMA busy, L1 / L2 / HBM):
 
-    python tools/exp_c3_clock.py fused [plies] [launches]   # C3 k_play launches (bench's form)
+    python tools/exp_c3_clock.py fused [plies] [launches] [c3|c2]   # k_play in bench's form
     python tools/exp_c3_clock.py iso [seconds] [boards]     # the trunk alone, back to back
 
 fused: 32,768 games x 800 sims, 10x128, memo + deferred last batch + table, groups of 16, the
@@ -26,20 +26,23 @@ import rvz  # noqa: E402
 from rvz import _lib  # noqa: E402
 
 
-def fused(plies=20, launches=2, games=32768, blocks=10, filters=128, group=-16):
+def fused(plies=20, launches=2, games=32768, blocks=10, filters=128, group=-16, board=8,
+          sims=800):
     import bench
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    net = rvz.AlphaZeroNetwork(8, blocks, filters).to(dev).eval()
-    eng = rvz.Engine(games, 800, 64, 1.0, board_size=8, device=dev, compact_leaves=True, memo=True)
+    net = rvz.AlphaZeroNetwork(board, blocks, filters).to(dev).eval()
+    eng = rvz.Engine(games, sims, 64, 1.0, board_size=board, device=dev, compact_leaves=True,
+                     memo=True)
     eng.table(1 << 20, 14)
     run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net, device=dev), temperature=1.0,
                              fused_softmax=True, autoreset=True, seed_base=42,
                              skip_last_eval=True, fused=True)
     run.play_group = group
     run.start()
-    bud = bench.stagger_budget(run.seeds - 42, 60, games, "blocked")
-    eng.play(run.evaluator, 59, 1.0, run.seeds, run.seed_stride, run._plies, run._done,
+    L = board * board - 4
+    bud = bench.stagger_budget(run.seeds - 42, L, games, "blocked")
+    eng.play(run.evaluator, L - 1, 1.0, run.seeds, run.seed_stride, run._plies, run._done,
              reset=True, skip_last_eval=True, games_per_workgroup=group, budget=bud)
     torch.cuda.synchronize()
     timer, stream = _lib.Timer(2 * launches), _lib.stream_handle(dev)
@@ -94,10 +97,17 @@ def iso(seconds=5.0, boards=32768, blocks=10, filters=128):
             "frac": round(fpr * boards / (avg * 1e-3) / 1e12 / 2500, 4)}
 
 
+CONFIGS = {"c3": dict(games=32768, blocks=10, filters=128, group=-16),
+           "c2": dict(games=4096, blocks=6, filters=64, group=-6),
+           "c5": dict(games=16384, blocks=6, filters=64, group=-24, board=6, sims=400)}
+
 if __name__ == "__main__":
     mode = sys.argv[1]
     if mode == "fused":
-        out = fused(*(int(a) for a in sys.argv[2:4]))
+        cfg = CONFIGS[sys.argv[4] if len(sys.argv) > 4 else "c3"]
+        out = fused(*(int(a) for a in sys.argv[2:4]), **cfg)
+        out["config"] = sys.argv[4] if len(sys.argv) > 4 else "c3"
+        out["lib"] = os.environ.get("RVZ_LIB", "in-tree")
     else:
         a = sys.argv[2:]
         out = iso(float(a[0]) if a else 5.0, int(a[1]) if len(a) > 1 else 32768)
