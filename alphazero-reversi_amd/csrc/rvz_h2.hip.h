@@ -610,14 +610,7 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
     const int kq = lane >> 4;                         // this lane's 8-channel slot in a k-step
     unsigned pmask[PTW];                              // valid taps in iteration order
 #pragma unroll
-    for (int u = 0; u < PTW; ++u) {
-        pmask[u] = G::taps(wt.px[u]);
-        // opaque per conv (NBOARD > 1): the per-tap, per-tile A addresses derive from it, and
-        // hoisted out of the residual loop they held 2 x 9 x PTW registers across the whole tower
-        // (k_play spilled them in the packed 6x6 geometry); one board per workgroup has the
-        // registers and forms them faster once
-        if constexpr (NBOARD > 1) asm volatile("" : "+v"(pmask[u]));
-    }
+    for (int u = 0; u < PTW; ++u) pmask[u] = G::taps(wt.px[u]);
     f32x4 acc[CTW][PTW];
 #pragma unroll
     for (int c = 0; c < CTW; ++c)
@@ -944,11 +937,19 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     // that overflowed set their bit in the pass's overflow word; RANGED true: a re-run for those
     // boards (mask) with the activation range scaled (ActRange), the others unscaled as before,
     // so every row's outputs still depend only on its own position
-    RangeS<NBOARD> simg =
-        grp1 ? h2_trunk<F, NBOARD, CTW, PTW, BS, ILV, 1, false>(smem, x, gb, bits, prm, L, blob,
-                                                                 n_blocks, tid, lane, wave, ovf, 0u)
-             : h2_trunk<F, NBOARD, CTW, PTW, BS, ILV, 0, false>(smem, x, gb, bits, prm, L, blob,
+    // (through a generic lambda: the same call written directly, or as a ?: pair, sends k_play's
+    // packed 6x6 instance into 276 B of spills and C2's into 36 B — the inliner's order decides
+    // which loop-invariant tap addresses stay hoisted; this form keeps round 4's codegen)
+    auto trunk = [&](auto grp) -> RangeS<NBOARD> {
+        constexpr int GR = decltype(grp)::value;
+        return h2_trunk<F, NBOARD, CTW, PTW, BS, ILV, GR, false>(smem, x, gb, bits, prm, L, blob,
                                                                  n_blocks, tid, lane, wave, ovf, 0u);
+    };
+    RangeS<NBOARD> simg;
+    if (grp1)
+        simg = trunk(std::integral_constant<int, 1>{});
+    else
+        simg = trunk(std::integral_constant<int, 0>{});
     // the overflow words are final after the tower's last barrier (n_blocks = 0: the stem's)
     const unsigned omask = rl.ov_all();
     if (omask != 0u) {                                // rare: re-run the boards that overflowed

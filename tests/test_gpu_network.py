@@ -77,10 +77,10 @@ def test_evaluator_fp32_matches_module(blocks, filters):
     assert (vb - vr).abs().mean().item() < 0.1      # tanh saturates: a few signs flip
 
 
-def _bn_net(blocks, filters, seed=3):
+def _bn_net(blocks, filters, seed=3, board=8):
     import rvz
     torch.manual_seed(seed)
-    net = rvz.AlphaZeroNetwork(8, blocks, filters).cuda().eval()
+    net = rvz.AlphaZeroNetwork(board, blocks, filters).cuda().eval()
     with torch.no_grad():
         for m in net.modules():
             if isinstance(m, torch.nn.BatchNorm2d):
@@ -203,11 +203,12 @@ def _fp32_module_err(net, x, l64, v64):
 
 @pytest.mark.parametrize("where", ["stem_bias", "tower_weights"])
 def test_h2_activation_range_is_scaled_not_overflowed(where):
-    """h2 keeps activations as two f16 parts, which overflow at 65520. Each
-    board's activation image is stored scaled by a power of two chosen from a bound on the
-    layer's outputs (ActRange, csrc/rvz_h2.hip.h), so a net whose activations reach ~1e5-1e7
-    evaluates fp32-class instead of raising: the stem bias at 1e5 (round 4's overflow case), or
-    the tower's conv weights scaled up so that activations grow block after block."""
+    """h2 keeps activations as two f16 parts, which overflow at 65520. A pass
+    whose unscaled trunk overflowed re-runs the boards that did with each board's activation
+    image stored scaled by a power of two chosen from a bound on the layer's outputs (h2_pass,
+    csrc/rvz_h2.hip.h), so a net whose activations reach ~1e5-1e7 evaluates fp32-class instead
+    of raising: the stem bias at 1e5 (round 4's overflow case), or the tower's conv weights
+    scaled up so that activations grow block after block."""
     import rvz
     net = _bn_net(2, 64, seed=6)
     x = (torch.rand(256, 3, 8, 8, device="cuda") > 0.6).float()
@@ -232,9 +233,9 @@ def test_h2_activation_range_is_scaled_not_overflowed(where):
 
 
 def test_h2_activation_range_leaves_ordinary_nets_bitwise():
-    """The range table's bounds stay below 2^15 for ordinary nets, so nothing is scaled: the
-    outputs are those of the unscaled arithmetic, which the fixture and fp32-class tests pin;
-    here: the blob's range table holds K = max over channels of sum |w| and Bb = max |bias| of
+    """Ordinary nets never overflow, so nothing is re-run or scaled: the outputs are those of the
+    unscaled arithmetic, which the fixture and fp32-class tests pin; here: the blob's range
+    table (the re-run's bounds) holds K = max over channels of sum |w| and Bb = max |bias| of
     every layer (BN folded), and a row's outputs do not depend on its pass partner."""
     import rvz
     from rvz.network import pack_resnet_params  # noqa: F401
@@ -394,3 +395,44 @@ def test_h2_unit_counter_any_start(board, filters, n):
             lg, vl = ev(x)
             assert torch.equal(lg, l0) and torch.equal(vl, v0), start
     assert not ev.overflowed()
+
+
+@pytest.mark.parametrize("board,blocks,filters", [(8, 2, 64), (6, 2, 64), (8, 1, 128)])
+def test_h2_range_rerun_is_per_board(board, blocks, filters):
+    """Passes that mix boards that overflow with boards that do not (every geometry: the 8x8
+    pair, three packed 6x6 boards, one 8x8 board at F = 128). The stem's weights on input plane
+    0 are scaled by 1e6, so a row overflows exactly when its plane 0 has a disc; half the rows
+    have an empty plane 0. Only the overflowed boards are re-run scaled: a quiet row's outputs
+    are bit for bit those of a batch of quiet rows only, a loud row's those of any other
+    pairing (the table and memo need a row's outputs to depend on its position alone), and the
+    loud rows are fp32-class against fp64."""
+    import rvz
+    net = _bn_net(blocks, filters, seed=9, board=board)
+    with torch.no_grad():
+        net.conv.weight[:, 0].mul_(1e6)
+    n = 96
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = (torch.rand(n, 3, board, board, device="cuda", generator=g) > 0.6).float()
+    loud = torch.arange(n, device="cuda") % 4 < 2                 # rows 0,1 4,5 ...: loud
+    x[~loud, 0] = 0.0
+    x[loud, 0, 0, 0] = 1.0                                        # at least one disc
+    ev = rvz.LeafEvaluator(net, kernel="h2")
+    lo, v = (t.clone() for t in ev(x))
+    assert not ev.overflowed()
+    q = torch.nonzero(~loud).flatten()
+    lq, vq = (t.clone() for t in ev(x[q].contiguous()))
+    assert torch.equal(lo[q], lq) and torch.equal(v[q], vq)
+    perm = torch.randperm(n, device="cuda", generator=g)
+    lp, vp = (t.clone() for t in ev(x[perm].contiguous()))
+    inv = torch.argsort(perm)
+    assert torch.equal(lp[inv], lo) and torch.equal(vp[inv], v)
+    l64, v64 = _fp64_outputs(net, x)
+    with torch.no_grad():                                         # the stems past f16's range
+        stem = torch.relu(net.bn(net.conv(x))).amax(dim=(1, 2, 3))
+    assert (stem[loud] > 65520).all() and (stem[~loud] < 100).all()
+    e32, ev32 = _fp32_module_err(net, x, l64, v64)
+    err = (lo.double().cpu() - l64).abs().max().item()
+    verr = (v.double().cpu() - v64).abs().max().item()
+    scale = l64.abs().max().item()
+    assert err <= 4 * e32 + 1e-6 * scale, (err, e32, scale)
+    assert verr <= 4 * ev32 + 1e-6, (verr, ev32)
