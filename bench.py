@@ -618,6 +618,25 @@ def stored_traffic(args, kernel, plies=None):
     return b, src
 
 
+def stored_pmc_clock(args):
+    """The k_play entry's PMC-pass clock and launch time (GRBM_GUI_ACTIVE / 8 / duration, the
+    same stored passes as its traffic; tools/pmc_play_traffic.py), for the configuration it was
+    measured on, else None."""
+    try:
+        pmc = json.load(open(args.pmc))
+    except Exception:
+        return None
+    key = f"play_{args.config}" if args.config != "c2" else "play"
+    ent = pmc.get(key, {})
+    if ent.get("config", "c2") != args.config or ent.get("games", 4096) != args.games:
+        return None
+    if "clock_GHz" not in ent:
+        return None
+    return {"clock_GHz": ent["clock_GHz"], "ms_per_launch": ent.get("ms_per_launch_clock_pass"),
+            "plies_per_launch": ent.get("plies_per_launch"),
+            "source": f"{os.path.relpath(args.pmc, ROOT)}[{key}] (not measured in this run)"}
+
+
 def selfplay(args, device, rank, world, full=True):
     """One workload (args: a resolved preset) on this rank: warm-up, the ply graph(s) captured,
     `steps` timed replays, the dominant kernel's in-situ roofline. With `full`, also the eager
@@ -817,6 +836,7 @@ def selfplay(args, device, rank, world, full=True):
             "useful_flops_per_row": upr,
             "useful_achieved": round(ach_u, 2), "useful_frac": round(ach_u / peak, 4),
             "traffic": traffic, "traffic_source": traffic_src,
+            "pmc_clock": stored_pmc_clock(args) if args.fused else None,
             "avg_ms_per_launch": round(t_tr, 4), "rows_per_launch": round(rows_tr, 1),
             "timing": timing, "isolated": iso,
             "live_rows_per_launch_timed": round(rows / nn_calls, 1),
