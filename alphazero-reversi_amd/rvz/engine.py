@@ -108,8 +108,8 @@ class Engine:
             of = getattr(ev, "overflowed", None)
             if of is not None and of():
                 raise RvzError(f"leaf evaluator ({getattr(ev, 'kernel', type(ev).__name__)}) "
-                               "overflowed its f16 activation range (|x| >= 65520): the NN "
-                               "outputs of the searches are not valid")
+                               "overflowed its f16 activation range (|x| >= 65520) even in the "
+                               "ranged re-run: the NN outputs of the searches are not valid")
 
     def counters(self) -> Tuple[int, int]:
         out = (C.c_int64 * 2)()

@@ -278,8 +278,9 @@ class LeafEvaluator:
         return w
 
     def overflowed(self) -> bool:
-        """True if any activation of any call so far reached the f16 range limit
-        (65520) — the outputs of that call are then not valid (synchronises)."""
+        """True if a call's activations stayed past the f16 range limit (65520) even after the
+        ranged re-run of the boards that reached it (a bound error; no finite net measured sets
+        it) — the outputs of that call are then not valid (synchronises)."""
         fused = getattr(self, "_ovf", None)
         return (any(bool(w[-4].item() != 0) for _, _, w in self._outs.values()) or
                 (fused is not None and bool(fused[0].item() != 0)))

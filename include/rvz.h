@@ -291,11 +291,16 @@ int rvz_resnet_heads_fc(int32_t board, const float *work, int32_t n, const float
  * x = x0 + x1 (f16 each, 22 significant bits), weights pre-scaled per output channel by a power
  * of two, the three partial products x0w0 + x0w1 + x1w0 accumulated in one fp32
  * accumulator (error of an fp32 GEMM; see csrc/rvz_resnet.hip k_resnet_h2). Boards 8 and 6.
- * blob: rvz_resnet_h2_weights' output (scaled f16 parts + inverse scales, once per parameter
- * update), rvz_resnet_h2_size(filters, blocks) uint16 elements, 16-byte aligned.
+ * blob: rvz_resnet_h2_weights' output (scaled f16 parts + inverse scales, then a range table of
+ * {max over output channels of sum |w|, max |bias|} per conv layer, once per parameter update),
+ * rvz_resnet_h2_size(filters, blocks) uint16 elements, 16-byte aligned.
+ * Activation range: a pass whose unscaled activations reach f16's limit (65520) re-runs the
+ * boards that did with their images scaled by a power of two chosen from the range table's
+ * bounds (exact; fp32-class relative to the board's largest activation); other boards' outputs
+ * are unchanged bit for bit.
  * work: rvz_resnet_work_size(n) floats (16-byte aligned); work[n * 192] (zero it before the first
- * use) is set to 1 (never cleared by the kernel) if an activation reached the f16 range limit
- * 65520, i.e. the outputs are not valid; words n * 192 + 2, 3 hold the trunk's 64-bit board-unit
+ * use) is set to 1 (never cleared by the kernel) if a scaled re-run still overflowed (a bound
+ * error: the outputs are not valid; no finite net reaches it); words n * 192 + 2, 3 hold the trunk's 64-bit board-unit
  * counter (units dealt to workgroups in start order; any initial value below 2^63). A misaligned
  * work returns RVZ_EINVAL. A workspace must not be shared by launches that can run concurrently
  * (two streams, or one buffer reused across overlapping launches): every launch claims its
