@@ -71,10 +71,10 @@ def test_fused_plays_the_runner_games(memo, skip):
 
 @pytest.mark.parametrize("gpw,chunks", [(1, (None,)), (3, (5, 1, 14)), (7, (20,)), (64, (20,)),
                                         (-1, (None,)), (-2, (20,)), (-3, (7, 13)), (-4, (9, 11)),
-                                        (-6, (20,)), (-8, (20,)), (-64, (20,))])
+                                        (-6, (20,)), (-8, (20,)), (-16, (9, 11)), (-64, (20,))])
 def test_fused_workgroup_sizes_and_launch_splits(gpw, chunks):
     """Static schedule with 1 / 3 / 7 / 64 games per workgroup (a partial last workgroup, odd
-    queues) and the task queue with groups of 1 / 2 / 3 / 4 / 6 / 8 / 64 games (a group's
+    queues) and the task queue with groups of 1 / 2 / 3 / 4 / 6 / 8 / 16 (C3's) / 64 games (a group's
     consecutive plies on different workgroups, published by agent-scope release / acquire), the
     plies split over several launches: the same games."""
     net = _net(8, 2, 64, seed=3)
