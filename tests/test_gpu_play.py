@@ -3,6 +3,7 @@ workgroup plays its own games â€” search, h2 trunk + FC heads, act, autoreset â€
 Held bit for bit against the pull-style runner (per-batch k_step / trunk / heads launches, k_act,
 k_autoreset), which the other GPU tests pin to the oracle and the reference's recorded games:
 every ply's move of every game, the final boards, statuses, RNG-driven restarts and counters."""
+import numpy as np
 import pytest
 import torch
 
@@ -124,3 +125,66 @@ def test_fused_graph_capture_and_errors():
     eng.search_step()
     with pytest.raises(rvz.RvzError):
         eng.play(run.evaluator, 1, 1.0, run.seeds, G, run._plies, run._done)
+
+
+@pytest.mark.parametrize("board,filters", [(8, 64), (6, 64), (8, 128)])
+def test_fused_ranged_rerun_is_per_board(board, filters):
+    """The activation range's re-run inside k_play (h2_pass: an unscaled trunk, then the boards
+    that overflowed again with their images scaled) keeps every board's outputs a function of
+    its own position: stem channels 0-7 fire at 2e5 (past f16's 65520) exactly where the mover
+    has >= 7 discs in a 3x3 window (and feed nothing but the skip path, so the games stay
+    ordinary), so mid-game passes mix overflowing and ordinary boards, and
+    the fused launch (queue groups, its own pass grouping) plays the same games, bit for bit, as
+    the pull-style runner (k_resnet_h2's pass grouping). Geometries: the 8x8 pair (C2), three
+    packed 6x6 boards (C5), one 8x8 board at F = 128 (C3)."""
+    net = _net(board, 2, filters, seed=2)
+    W = 2e5
+    with torch.no_grad():
+        net.conv.weight[:8].zero_()
+        net.conv.weight[:8, 0] = W
+        if net.conv.bias is not None:
+            net.conv.bias[:8].zero_()
+        net.bn.running_mean[:8] = 0.0
+        net.bn.running_var[:8] = 1.0 - net.bn.eps
+        net.bn.weight[:8] = 1.0
+        net.bn.bias[:8] = -6.5 * W
+        # the loud channels reach no other channel and no head (they ride the skip path): the
+        # games stay ordinary, only the stored images carry the large values
+        for blk in net.res_blocks:
+            blk.conv1.weight[:, :8] = 0.0
+        for m in (net.policy_conv, net.value_conv):
+            m.weight[:, :8] = 0.0
+    # S = 320: five batches, so a search's visits spread over several root children (with two,
+    # every copy of the second batch takes the first unvisited child: mcts.py's +inf for N = 0)
+    # and the games' sampled moves diverge
+    G, S, plies = 192, 320, (56 if board == 8 else 28)
+    n = board * board
+    bits = np.arange(n, dtype=np.uint64)
+
+    def loud_boards(eng):      # boards whose mover has a window of >= 7 discs (stem past 65520)
+        state = eng.get_state()
+        torch.cuda.synchronize()                  # (copied on the engine's stream)
+        bl, wh, st = (t.cpu().numpy() for t in state)
+        mover = np.where((st[:, 0] == 1)[:, None], bl.view(np.uint64)[:, None],
+                         wh.view(np.uint64)[:, None])
+        grid = ((mover >> bits) & np.uint64(1)).astype(np.int32).reshape(G, board, board)
+        pad = np.pad(grid, ((0, 0), (1, 1), (1, 1)))
+        win = sum(pad[:, 1 + dr:1 + dr + board, 1 + dc:1 + dc + board]
+                  for dr in (-1, 0, 1) for dc in (-1, 0, 1))
+        return int((win >= 7).any(axis=(1, 2)).sum())
+
+    import rvz
+    run = rvz.SelfPlayRunner(rvz.Engine(G, S, 64, board_size=board, compact_leaves=True, memo=True),
+                             rvz.LeafEvaluator(net), autoreset=True, seed_base=42,
+                             skip_last_eval=True)
+    run.start()
+    moves, counts = [], []
+    for _ in range(plies):
+        run.ply()
+        moves.append(run.eng.idx_buf.clone())
+        counts.append(loud_boards(run.eng))       # roots of the next search: some loud, some not
+    assert sum(0 < c < G for c in counts) >= 3, str(counts)
+    a = _fused(net, G, S, plies, True, True)
+    _same(a, (run, torch.stack(moves)))
+    for r in (a[0], run):
+        assert not r.evaluator.overflowed()
