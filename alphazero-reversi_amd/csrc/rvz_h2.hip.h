@@ -42,7 +42,7 @@ namespace {
 //   [H2_PAD k-steps of zeros: the prefetch past the last layer]
 //   [stem frags: part][ctile][lane][8]  (K = 27 padded to 32, k = tap*3 + ch)
 //   [inverse scales: float[1 + 2*NB][F]: stem, then the trunk layers]
-//   [activation ranges: float[1 + 2*NB][2] {K, Bb} (h2_range_off; ActRange below)]
+//   [activation ranges: float[1 + 2*NB][2] {K, Bb} (h2_range_off; the activation range section below)]
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
@@ -313,7 +313,7 @@ __device__ __forceinline__ void load_epi(EpiH<CTW, PTW>& er, const float* __rest
 
 // v = acc * isc + bias (+ skip), ReLU, split into the two parts: the lane holds 4 consecutive
 // channels of one pixel per tile -> two 8-byte writes.
-// Activation range (ActRange above), two modes. RANGED false (every pass first): the values are
+// Activation range (the section above), two modes. RANGED false (every pass first): the values are
 // stored unscaled, and a board with a value past f16's range sets its bit in the pass's overflow
 // word *ovw (LDS; a wave-uniform test, one compare per value as the sticky flag always cost).
 // RANGED true (only a pass whose word is set, re-run for those boards): the accumulator is
@@ -751,9 +751,11 @@ struct HeadsInLds {
 
 // The stem and the residual tower of one pass (h2_pass). RG (RANGED) false: every pass, values
 // stored unscaled, boards that overflowed set their bit in the pass's overflow words; RG true: a
-// re-run for those boards (mask) with the activation range scaled (ActRange), the others
-// unscaled as before, so every row's outputs still depend only on its own position. GR: the
-// ILV pixel group (conv_h2's tile-0 skip window). Returns the final image's scale exponents.
+// re-run for those boards (mask) with the activation range scaled (RangeS), the others
+// unscaled as before, so every row's outputs still depend only on its own position (the re-run
+// prefetches one k-step of weights and no activations: its speed does not matter and its stack
+// stays small). GR: the ILV pixel group (conv_h2's tile-0 skip window). Returns the final
+// image's scale exponents.
 template <int F, int NBOARD, int CTW, int PTW, int BS, bool ILV, int GR, bool RG>
 __device__ __forceinline__ RangeS<NBOARD> h2_trunk(char* smem, const float* __restrict__ x,
                                                    const int (&gb)[NBOARD], const uint64_t* bits,
@@ -951,7 +953,7 @@ __device__ __forceinline__ void h2_pass(char* smem, const float* __restrict__ x,
     if (lane == 0) *rl.ovw(wave) = 0u;                // this wave's overflow word (its epilogues)
     // the stem and the residual tower. RANGED false: every pass, values stored unscaled, boards
     // that overflowed set their bit in the pass's overflow word; RANGED true: a re-run for those
-    // boards (mask) with the activation range scaled (ActRange), the others unscaled as before,
+    // boards (mask) with the activation range scaled (RangeS), the others unscaled as before,
     // so every row's outputs still depend only on its own position
     // (through a generic lambda: the same call written directly, or as a ?: pair, sends k_play's
     // packed 6x6 instance into 276 B of spills and C2's into 36 B — the inliner's order decides
