@@ -220,7 +220,7 @@ def test_fused_records_equal_the_pull_style_records(table):
     from rvz.trainer import records_to_training
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 2, 64).cuda().eval()
-    G, S, P = 160, 128, 60
+    G, S, P = 160, 200, 60     # four batches: distinct games per slot
     runs = []
     for fused in (False, True):
         eng = rvz.Engine(G, S, 64, compact_leaves=True, memo=True)

@@ -79,9 +79,11 @@ def test_fused_workgroup_sizes_and_launch_splits(gpw, chunks):
     consecutive plies on different workgroups, published by agent-scope release / acquire), the
     plies split over several launches: the same games."""
     net = _net(8, 2, 64, seed=3)
-    G, S = 203, 128
-    _same(_fused(net, G, S, 20, True, True, gpw=gpw, chunks=chunks),
-          _plain(net, G, S, 20, True, True))
+    G, S = 203, 200       # four batches: the games' sampled moves diverge (with two, every copy
+    # of the second batch takes the first unvisited child and the slots play one game)
+    a = _fused(net, G, S, 20, True, True, gpw=gpw, chunks=chunks)
+    assert len(set(a[1][3].tolist())) > 1                  # distinct games by the fourth ply
+    _same(a, _plain(net, G, S, 20, True, True))
 
 
 @pytest.mark.parametrize("board,blocks,filters,gpw", [(8, 2, 128, 0), (8, 2, 128, -16),

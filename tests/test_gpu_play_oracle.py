@@ -157,7 +157,7 @@ def test_ply_budget_plays_prefixes(gpw):
     alone; its moves are the first budget[g] of an unbudgeted run, and topping the budgets up to
     the same total afterwards gives the unbudgeted run's games exactly (queue and static)."""
     net = _net(8, 2, 64, seed=5)
-    G, S, P = 203, 128, 9
+    G, S, P = 203, 200, 9      # four batches: distinct games per slot
     full = _fused_runner(net, G, S, gpw=gpw)
     hf = _play(full, P)
     bud = torch.arange(G, dtype=torch.int32, device="cuda") % (P + 2) - 1   # -1 .. P

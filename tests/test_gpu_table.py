@@ -74,7 +74,7 @@ def test_table_tiny_full_or_static(slots, discs, gpw):
 @pytest.mark.parametrize("board,blocks,filters", [(6, 2, 64), (8, 2, 128)])
 def test_table_other_geometries(board, blocks, filters):
     net = _net(board, blocks, filters, seed=1)
-    G, S, P = 160, 128, 34
+    G, S, P = 160, 200, 34     # four batches: distinct games per slot
     _same(_run(net, G, S, P, table=(1 << 14, 14), chunks=[10, 24]), _run(net, G, S, P))
 
 
