@@ -1376,6 +1376,23 @@ int rvz_env_set(rvz_engine* e, const uint64_t* black, const uint64_t* white, con
     return RVZ_OK;
 }
 
+int rvz_env_set_draws(rvz_engine* e, const double* u) {
+    static_assert(RNG_DRAWS == RVZ_DRAWS, "include/rvz.h's RVZ_DRAWS is the stream length");
+    if (!e || !u) return RVZ_EINVAL;
+    const size_t G = e->v.G;
+    RVZ_HIP(hipMemcpyAsync(e->v.rng_u, u, G * RNG_DRAWS * sizeof(double), hipMemcpyDeviceToDevice,
+                           e->stream), e);
+    RVZ_HIP(hipMemsetAsync(e->v.rng_pos, 0, G * sizeof(int32_t), e->stream), e);
+    return RVZ_OK;
+}
+
+int rvz_env_draws(rvz_engine* e, int32_t* out_pos) {
+    if (!e || !out_pos) return RVZ_EINVAL;
+    RVZ_HIP(hipMemcpyAsync(out_pos, e->v.rng_pos, (size_t)e->v.G * sizeof(int32_t),
+                           hipMemcpyDeviceToDevice, e->stream), e);
+    return RVZ_OK;
+}
+
 int rvz_board_legal(int32_t bs, int32_t n, const uint64_t* black, const uint64_t* white,
                     const int32_t* status, uint64_t* out, void* stream) {
     if ((bs != 8 && bs != 6) || n < 0 || (n > 0 && (!black || !white || !status || !out)))

@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("RVZ_LIB", os.path.join(_HERE, "librvz.so"))   # RVZ_L
 
 RVZ_OK, RVZ_DONE = 0, 1
 RVZ_LEAF_F32, RVZ_LEAF_BF16 = 0, 1
+RVZ_DRAWS = 64          # move-sampling draws held per game (rvz_env_set_draws)
 
 
 class RvzError(RuntimeError):
@@ -42,6 +43,8 @@ SIGNATURES = {
     "rvz_sync": (C.c_int, [_P]),
     "rvz_check": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "rvz_env_reset": (C.c_int, [_P, _P, _P]),
+    "rvz_env_set_draws": (C.c_int, [_P, _P]),
+    "rvz_env_draws": (C.c_int, [_P, _P]),
     "rvz_env_get": (C.c_int, [_P, _P, _P, _P]),
     "rvz_env_set": (C.c_int, [_P, _P, _P, _P]),
     "rvz_env_legal": (C.c_int, [_P, _P]),

@@ -183,6 +183,23 @@ class Engine:
         self._call("rvz_env_autoreset", ptr(idx), ptr(seeds), int(stride), ptr(plies), ptr(done),
                    int(bool(reset)))
 
+    def set_draws(self, u: torch.Tensor):
+        """rvz_env_set_draws: game g's move-sampling draws become u[g] (float64 [G, RVZ_DRAWS],
+        the values np.random.random_sample() would return), each game rewound to its first."""
+        uu = u.to(self.device, torch.float64).contiguous()
+        if uu.shape != (self.n_games, _lib.RVZ_DRAWS):
+            raise RvzError(f"set_draws: u must be float64 [{self.n_games}, {_lib.RVZ_DRAWS}]")
+        self._stream()
+        self._call("rvz_env_set_draws", ptr(uu))
+        self._draws_keep = uu          # the copy is stream-ordered: keep the source alive
+
+    def draws(self) -> torch.Tensor:
+        """rvz_env_draws: the draws each game consumed since its reset / set_draws (int32 [G])."""
+        out = torch.empty(self.n_games, dtype=torch.int32, device=self.device)
+        self._stream()
+        self._call("rvz_env_draws", ptr(out))
+        return out
+
     def get_state(self):
         """(black int64[G], white int64[G], status int32[G,4]) device tensors (bit patterns)."""
         self._stream()

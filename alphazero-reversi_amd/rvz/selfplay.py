@@ -300,13 +300,37 @@ class LaneRunner:
 
 
 class SelfPlay:
-    """self_play.py:21-219 with the games of one call played in lockstep on the GPU."""
+    """self_play.py:21-219 with the games of one call played in lockstep on the GPU.
+
+    Randomness. The reference samples every move with np.random.choice (mcts.py:684), i.e. one
+    random_sample() from NumPy's GLOBAL stream per move at temperature > 0, and plays the games
+    of one generate_games call one after another (self_play.py:66-101); the stream is seeded once
+    per pipeline (pipeline.py:74-80) and SelfPlay takes no seed (pipeline.py:152-168). By default
+    this class draws exactly that: game k's moves take the k-th contiguous piece of the caller's
+    np.random stream, and np.random is left where the sequential loop leaves it. The lockstep
+    games cannot know in advance where their piece starts (it depends on the earlier games'
+    lengths), so the call plays passes (as rvz.arena does for tournaments): every game first
+    assumes that each earlier game drew bs*bs - 4 values (a full board; true of all but ~0.1 %
+    of games), the games are played in lockstep with their pieces handed to the engine
+    (Engine.set_draws), each game's actual draw count is read back (Engine.draws), and only the
+    games whose start offset changed are played again. A game's moves are a function of its
+    piece alone (searches are per game, bit for bit), game 0's offset is always exact, and once
+    games 0..k are exact so is game k + 1, so the passes end; `reference_order_passes` reports
+    the count (1 unless an earlier game ended before the board was full).
+
+    args["seed"] (opt-in, the round 1-5 behaviour): game i of the j-th game played by this
+    object instead draws from its own np.random.seed(seed + j) stream, and np.random is not
+    touched.
+    """
 
     def __init__(self, model, args: dict, evaluator: Optional[Callable] = None):
         """evaluator: the leaf evaluator (default: LeafEvaluator(model), the fp32 h2 kernel).
         Any callable leaf_x -> (logits, value) works; with ``outputs_probs = True`` it returns
         softmaxed rows instead of logits, and a ``bind(engine)`` method is called with each new
-        engine (tests replay the reference's recorded NN outputs this way)."""
+        engine (tests replay the reference's recorded NN outputs this way).
+        args["fused"] (default False): with the h2 LeafEvaluator, every game of a pass is played
+        to its end in ONE rvz_play launch (Engine.play) instead of the pull-style ply loop; the
+        same games."""
         from .network import LeafEvaluator
         self.model = model
         self.device = next(model.parameters()).device
@@ -320,10 +344,19 @@ class SelfPlay:
         self.board_size = int(getattr(model, "board_size", 8))
         self.save_dir = args.get("save_dir", "self_play_data")
         os.makedirs(self.save_dir, exist_ok=True)
-        self.seed = int(args.get("seed", 42))
+        self.seed = None if args.get("seed") is None else int(args["seed"])
+        self.fused = bool(args.get("fused", False))
+        if self.fused and not isinstance(self.evaluator, LeafEvaluator):
+            raise ValueError("SelfPlay: args['fused'] plays the h2 LeafEvaluator inside the "
+                             "launch; another evaluator goes through the pull-style loop")
         self.games_played = 0
+        self.reference_order_passes = 0
 
-    def _play(self, num_games: int) -> List[Dict]:
+    def _run(self, num_games: int, seed_base: int, draws: Optional[np.ndarray] = None):
+        """Play num_games fresh games to their end; draws (float64 [num_games, RVZ_DRAWS]):
+        each game's move-sampling values (None: game i draws from np.random.seed(seed_base + i)).
+        Returns the records (rec_black, rec_white, rec_side, rec_idx [P, G], rec_p [P, G, npol],
+        final status [G, 4]) and the draws each game consumed (int32 [G], host)."""
         # compacted leaf batches: only the live leaves are evaluated (as _process_batch does);
         # the NN-output memo (Engine.memo) with the default evaluator, whose rows depend only on
         # the position; the games are identical either way
@@ -340,22 +373,95 @@ class SelfPlay:
         max_plies = bs * bs - 4         # every ply places a disc (passes are inside make_move)
         run = SelfPlayRunner(eng, self.evaluator, self.args.get("temperature", 1.0),
                              fused_softmax=self.args.get("fused_softmax", True),
-                             seed_base=self.seed + self.games_played, record=True,
-                             max_plies=max_plies)
+                             seed_base=seed_base, record=True, max_plies=max_plies,
+                             fused=self.fused)
         run.start()
-        for _ in range(max_plies):
-            run.ply()
+        if draws is not None:
+            eng.set_draws(torch.from_numpy(np.ascontiguousarray(draws, np.float64)))
+        if self.fused:
+            run.play_record(max_plies)
+        else:
+            for _ in range(max_plies):
+                run.ply()
         run.check()
         if not bool(run.post_status[:, 1].all()):
             raise RuntimeError(f"SelfPlay: a game is not over after {max_plies} plies")
-        G, P = num_games, max_plies
-        black, white, side = run.rec_black, run.rec_white, run.rec_side
+        used = eng.draws().cpu().numpy()
+        return (run.rec_black, run.rec_white, run.rec_side, run.rec_idx, run.rec_p,
+                run.post_status.clone()), used
+
+    def _play_reference_order(self, num_games: int):
+        """The passes of the class docstring over NumPy's global stream. Returns (records of
+        every pass, game -> (pass, column))."""
+        from ._lib import RVZ_DRAWS
+        T = float(self.args.get("temperature", 1.0))
+        passes, where, _ = sequential_draw_passes(
+            num_games, self.board_size ** 2 - 4, RVZ_DRAWS, T > 0, np.random,
+            lambda U: self._run(len(U), 0, draws=U))
+        self.reference_order_passes = len(passes)
+        return passes, where
+
+
+def sequential_draw_passes(num_games: int, max_draws: int, piece: int, draws_on: bool, rng,
+                           play: Callable):
+    """Lockstep passes that give every game the piece of ONE random_sample() stream it would
+    draw if the games ran one after another (SelfPlay's class docstring; self_play.py:66-101
+    with mcts.py:684). rng: a NumPy RandomState or the np.random module (its state is read once
+    and advanced at the end by exactly the values the sequential loop draws). A game draws at
+    most max_draws values (one per move; none when draws_on is False, i.e. temperature 0,
+    mcts.py:679-681). play(U float64 [k, piece]) plays k fresh games, game j drawing U[j, 0],
+    U[j, 1], ... in order, and returns (payload, used int [k]: the values each game drew).
+    Returns (payloads of every pass, game -> (pass, index in that pass), draws per game)."""
+    G = int(num_games)
+    rs = np.random.RandomState()
+    rs.set_state(rng.get_state())
+    stream = rs.random_sample(G * max_draws + piece)
+    n = np.full(G, max_draws if draws_on else 0, np.int64)   # first guess: the longest game
+    prev: List[Optional[int]] = [None] * G
+    where: List = [None] * G
+    payloads = []
+    while True:
+        off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
+        todo = [g for g in range(G) if prev[g] != int(off[g])]
+        if not todo:
+            break
+        payload, used = play(np.stack([stream[off[g]:off[g] + piece] for g in todo]))
+        for j, g in enumerate(todo):
+            if not 0 <= int(used[j]) <= max_draws:
+                raise RuntimeError(f"game drew {int(used[j])} values (at most {max_draws})")
+            n[g], prev[g], where[g] = int(used[j]), int(off[g]), (len(payloads), j)
+        payloads.append(payload)
+    total = int(n.sum())
+    if total:                       # leave the stream where the sequential loop leaves it
+        rng.random_sample(total)
+    return payloads, where, n
+
+    def _play(self, num_games: int) -> List[Dict]:
+        if num_games <= 0:
+            self._last_records = None
+            return []
+        if self.seed is not None:
+            recs, _ = self._run(num_games, self.seed + self.games_played)
+            passes, where = [recs], [(0, g) for g in range(num_games)]
+            self.reference_order_passes = 0
+        else:
+            passes, where = self._play_reference_order(num_games)
+        # one record set in game order: the columns of the pass that last played each game
+        base = np.concatenate([[0], np.cumsum([r[3].shape[1] for r in passes])[:-1]])
+        col = torch.tensor([int(base[p]) + j for p, j in where], device=self.device)
+        recs = [torch.cat([r[i] for r in passes], dim=1).index_select(1, col)
+                for i in range(5)]
+        recs.append(torch.cat([r[5] for r in passes], dim=0).index_select(0, col))
+        self._last_records = recs
+        bs = self.board_size
+        G, P = num_games, bs * bs - 4
+        black, white, side, idx_t, p_t, final_t = recs
         st = torch.stack([side, torch.zeros_like(side), torch.full_like(side, -1),
                           torch.zeros_like(side)], dim=-1).reshape(-1, 4).contiguous()
         planes = board_canonical(black.reshape(-1).contiguous(), white.reshape(-1).contiguous(),
                                  st, bs).reshape(P, G, 3, bs, bs)
-        planes, idx, p = planes.cpu().numpy(), run.rec_idx.cpu().numpy(), run.rec_p.cpu().numpy()
-        side_h, final = side.cpu().numpy(), run.post_status.cpu().numpy()
+        planes, idx, p = planes.cpu().numpy(), idx_t.cpu().numpy(), p_t.cpu().numpy()
+        side_h, final = side.cpu().numpy(), final_t.cpu().numpy()
         games = []
         for g in range(G):
             live = np.flatnonzero(idx[:, g] >= 0)
@@ -366,15 +472,14 @@ class SelfPlay:
                           "action_probs": [p[k, g] for k in live],
                           "current_players": players, "values": values, "winner": winner})
         self.games_played += G
-        self._last_run = run
         return games
 
     def training_tensors(self) -> Dict[str, torch.Tensor]:
         """The last call's games as device training arrays (rvz.trainer.records_to_training)."""
         from .trainer import records_to_training
-        run = self._last_run
-        return records_to_training(run.rec_black, run.rec_white, run.rec_side, run.rec_idx,
-                                   run.rec_p, run.post_status, run.eng.board_size)
+        if getattr(self, "_last_records", None) is None:
+            raise ValueError("SelfPlay.training_tensors: no games played by the last call")
+        return records_to_training(*self._last_records, self.board_size)
 
     def generate_games(self, num_games: int) -> List[Dict]:
         t0 = time.time()

@@ -277,7 +277,8 @@ def dry_run(args, rank, world, backend):
     for g in range(a, b):                    # stand-in work, proportional to the shard
         acc += sum(range(200)) + g
     dt = max(time.perf_counter() - t0, 1e-9)
-    rep = rdist.rank_report(rank_fields(rank, a, b, b - a, dt, None, "cpu (dry run)"))
+    rep = rdist.rank_report(rank_fields(rank, a, b, b - a, dt, None, "cpu (dry run)",
+                                        **stagger_fields(args)))
     if rank == 0:
         emit({"metric": "dry-run (launcher check)", "n_gpus": world, "rccl_world": world,
               "dist_backend": backend, "games_per_gpu": args.games,
@@ -287,12 +288,28 @@ def dry_run(args, rank, world, backend):
     tdist.destroy_process_group()
 
 
-def rank_fields(rank, first_game, end_game, plies, seconds, rows_per_ply, device):
+def rank_fields(rank, first_game, end_game, plies, seconds, rows_per_ply, device, **extra):
     """One rank's part of a line: its global game range, committed plies, timed seconds, its own
-    rate and NN rows per ply (rvz.dist.rank_report gathers them and their spread)."""
-    return {"rank": rank, "games": [first_game, end_game], "plies": int(plies),
-            "seconds": round(seconds, 9), "value": round(plies / seconds, 2) if seconds > 0 else None,
-            "nn_rows_per_ply": rows_per_ply, "device": str(device), "pid": os.getpid()}
+    rate and NN rows per ply (rvz.dist.rank_report gathers them and their spread), plus extra
+    fields (the stagger's ply range, table hits per ply)."""
+    return dict({"rank": rank, "games": [first_game, end_game], "plies": int(plies),
+                 "seconds": round(seconds, 9),
+                 "value": round(plies / seconds, 2) if seconds > 0 else None,
+                 "nn_rows_per_ply": rows_per_ply, "device": str(device), "pid": os.getpid()},
+                **extra)
+
+
+def stagger_fields(args):
+    """A rank's stagger, for its report: the plies its shard's games start at (every rank covers
+    0..L-1) and the fewest / most games at one ply."""
+    if args.no_stagger:
+        return {"stagger_plies": None}
+    L = args.board * args.board - 4
+    bud = stagger_budget(torch.arange(args.games, dtype=torch.int64), L, args.games,
+                         args.stagger_order)
+    cnt = torch.bincount(bud.long(), minlength=L)
+    return {"stagger_plies": [int(bud.min()), int(bud.max())],
+            "stagger_games_per_ply": [int(cnt.min()), int(cnt.max())]}
 
 
 # ------------------------------------------------------------------------------ measurement
@@ -344,21 +361,25 @@ def dispatch_summary():
     return out or None
 
 
-def stagger_budget(gidx: torch.Tensor, L: int, n_global: int, order: str) -> torch.Tensor:
-    """The ply of its game each global game index starts the run at (the stagger launch's
-    per-game budgets): blocked floor(g * L / N), interleaved g mod L."""
-    bud = gidx * L // n_global if order == "blocked" else gidx % L
+def stagger_budget(idx: torch.Tensor, L: int, n: int, order: str) -> torch.Tensor:
+    """The ply of its game each game of a rank's shard starts the run at (the stagger launch's
+    per-game budgets), from the game's index in the shard: blocked floor(i * L / n), interleaved
+    i mod L."""
+    bud = idx * L // n if order == "blocked" else idx % L
     return bud.to(torch.int32).contiguous()
 
 
-def stagger(args, runners, tag, device, world=1):
+def stagger(args, runners, tag, device, first_game=0):
     """Phase-neutral start: every game begins at the start position together,
     and 99.9% of 8x8 games last exactly 60 plies, so without this the games stay in lockstep and a
     window of fewer than 60 plies samples one game phase. One rvz_play launch with per-game ply
-    budgets puts global game g of N at ply floor(g * L / N) (--stagger-order blocked, the
-    default) or g mod L (interleaved) of its first game (L = S*S - 4 = 60 on 8x8, the length of
-    a full game): from then on every ply of the run holds a whole game's mix of phases, as
-    continuous self-play does (self_play.py:80-101), with N / L games at every ply either way.
+    budgets puts game i of the rank's n = --games at ply floor(i * L / n) (--stagger-order
+    blocked, the default) or i mod L (interleaved) of its first game (L = S*S - 4 = 60 on 8x8,
+    the length of a full game): from then on every ply of the run holds a whole game's mix of
+    phases, as continuous self-play does (self_play.py:80-101), with n / L games at every ply
+    either way. The index is the game's place in THIS rank's shard (indexing
+    the global game space gave rank r only plies [60 r / W, 60 (r + 1) / W), so rank 0 played
+    openings and rank W - 1 endgames): every rank holds the same mix of phases, whatever W.
     Blocked keeps the games of one fused-launch group (consecutive games) at one ply, as
     self-play's lockstep start does (one box: +0.8% / +0.9% in 20- / 60-ply windows,
     profiles/r04o_ab_stagger_order_*). Runs on each lane's engine (the pull-style presets
@@ -366,11 +387,11 @@ def stagger(args, runners, tag, device, world=1):
     tests/test_gpu_play_oracle.py::test_stagger_then_pull_style_equals_fused). Returns the mean
     plies per game it played."""
     L = args.board * args.board - 4
-    n_global = args.games * world
     disp = Dispatches(play_kernel(args.board, args.filters), device, n=len(runners))
     tot, n = 0, 0
     for r in runners:
-        bud = stagger_budget(r.seeds - args.seed, L, n_global, args.stagger_order)
+        # a lane's seeds are args.seed + its global game indices (seed_base + lane offset)
+        bud = stagger_budget(r.seeds - args.seed - first_game, L, args.games, args.stagger_order)
         tot += int(bud.sum().item())
         n += bud.numel()
         disp(f"{tag}stagger", lambda r=r, bud=bud: r.eng.play(
@@ -692,7 +713,8 @@ def selfplay(args, device, rank, world, full=True):
     stagger_plies = 0.0
     if not args.no_stagger:
         stagger_plies = stagger(args, [lane0] if args.fused else
-                                (run.runners if args.lanes > 1 else [run]), tag, device, world)
+                                (run.runners if args.lanes > 1 else [run]), tag, device,
+                                first_game)
 
     # warmup: the first ply eager, then capture the ply graph with lane 0's trunk launches
     # stamping a ring of per-workgroup device wall-clock stamps, one row per launch (the heads
@@ -776,12 +798,18 @@ def selfplay(args, device, rank, world, full=True):
     total, dt, value = rdist.aggregate_rate(s1 - s0, t1 - t0)
     # leaf rows evaluated per NN call in the timed region (compaction on), else the full batch
     # (a last batch left to the memo, --evals lazy, is not an NN call)
-    calls_per_search = [e.n_batches - (1 if args.skip_last_eval else 0) for e in engines]
+    # (a one-batch search evaluates its batch even with skip_last_eval: Engine.search, rvz_play)
+    calls_per_search = [e.n_batches - (1 if args.skip_last_eval and e.n_batches > 1 else 0)
+                        for e in engines]
     nn_calls = args.steps * sum(calls_per_search)
     rows = rows1 - rows0 if not args.no_compact else nn_calls * eng.n_games
     # every rank's own plies, seconds, rate and rows per ply, and their spread (rank 0 prints)
-    ranks = rdist.rank_report(rank_fields(rank, first_game, first_game + args.games, s1 - s0,
-                                          t1 - t0, round(rows / max(1, s1 - s0), 3), device))
+    ranks = rdist.rank_report(
+        rank_fields(rank, first_game, first_game + args.games, s1 - s0, t1 - t0,
+                    round(rows / max(1, s1 - s0), 3), device, **stagger_fields(args),
+                    table_hits_per_ply=(round(tab_d[0] / max(1, s1 - s0), 3)
+                                        if tab_d is not None and args.table else None)),
+        keys=("value", "seconds", "nn_rows_per_ply", "table_hits_per_ply"))
     trunk_live = None
     if graph_events:
         trunk_live = trunk_spans(graph_events[0], int(graph_events[1].item()))

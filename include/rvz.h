@@ -78,6 +78,17 @@ int rvz_env_reset(rvz_engine *e, const uint32_t *seeds, const uint8_t *mask);
  * out_idx; plies, done: int64 [n_games] per-game counters (sum them to read totals). */
 int rvz_env_autoreset(rvz_engine *e, const int32_t *idx, int64_t *seeds, int64_t stride,
                       int64_t *plies, int64_t *done, int32_t reset);
+/* The move-sampling draws of each game (np.random.choice's one random_sample() per move,
+ * mcts.py:684): rvz_env_reset fills game g's RVZ_DRAWS values from np.random.seed(seeds[g]);
+ * rvz_env_set_draws replaces them with u[g][0..RVZ_DRAWS) (float64, device) and rewinds every
+ * game to its first value, so a caller can hand each game its slice of ONE stream — the
+ * reference's generate_games draws every game's moves in sequence from the global np.random
+ * state (self_play.py:66-101, seeded once at pipeline.py:74-80). rvz_env_draws writes the number
+ * of values each game has consumed since then (int32 [n_games]; rvz_act / rvz_play at
+ * temperature 0 draw none). A game that would draw more than RVZ_DRAWS sets device error bit 1. */
+#define RVZ_DRAWS 64
+int rvz_env_set_draws(rvz_engine *e, const double *u);
+int rvz_env_draws(rvz_engine *e, int32_t *out_pos);
 int rvz_env_get(rvz_engine *e, uint64_t *black, uint64_t *white, int32_t *status);
 int rvz_env_set(rvz_engine *e, const uint64_t *black, const uint64_t *white, const int32_t *status);
 /* ReversiGame.get_valid_moves (game.py:72-79 -> board.py:70-133) as a bitmask per game */

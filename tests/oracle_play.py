@@ -50,3 +50,38 @@ class OracleGames:
 
     def winners(self):
         return [g.winner if g.over else None for g in self.games]
+
+
+def reference_generate_games(O, num_games: int, sims: int, temperature: float, rng, evaluate,
+                             bs: int = 8, batch: int = 64, c_puct: float = 1.0):
+    """SelfPlay.generate_games as the reference runs it (self_play.py:66-126), on the CPU oracle:
+    one game after another, each ply one MCTS search (mcts.py:322-407) whose leaves `evaluate`
+    answers (planes f32 [n, 3, bs, bs] -> (softmaxed rows f32 [n, npol], values f32 [n])), then
+    get_action_probs' tail (mcts.py:642-694) drawing its np.random.choice value from ONE stream
+    `rng` (a RandomState standing in for NumPy's global state, seeded once as pipeline.py:74-80
+    seeds it), the record of the position before the move, make_move. Returns the per-game dicts
+    (states, action_probs, current_players, values, winner, moves)."""
+    out = []
+    for _ in range(num_games):
+        game = O.new_game(bs)
+        d = {"states": [], "action_probs": [], "current_players": [], "moves": []}
+        while not game.over:
+            srch = O.Search(1, sims, batch, c_puct, bs=bs)
+            srch.begin([game])
+            while (r := srch.step()) is not None:
+                p, v = evaluate(O.leaf_planes(r[0], bs))
+                srch.submit(p, v)
+            vis = srch.visits()[0]
+            u = float(rng.random_sample()) if O.action_needs_draw(vis, temperature) else 0.0
+            a, p, _ = O.action(vis, temperature, u)
+            d["states"].append(O.canonical(game, bs))
+            d["current_players"].append(int(game.side))
+            d["action_probs"].append(p)
+            d["moves"].append(a)
+            assert O.make_move(game, -1 if a == bs * bs else a, bs)
+        w = int(game.winner)
+        d["winner"] = w
+        d["values"] = [0.0 if w == 0 else (1.0 if pl == w else -1.0)
+                       for pl in d["current_players"]]
+        out.append(d)
+    return out

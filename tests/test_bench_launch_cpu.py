@@ -164,22 +164,34 @@ def test_spawn_ranks_terminates_children_when_the_launcher_is_killed(tmp_path):
 
 
 @pytest.mark.parametrize("order", ["blocked", "interleaved"])
-@pytest.mark.parametrize("n,L,world", [(4096, 60, 1), (16384, 32, 1), (32768, 60, 8), (1000, 60, 2)])
-def test_stagger_budgets_are_phase_neutral(order, n, L, world):
-    """bench.py's stagger: every ply of the game holds N / L games (floor or
-    ceil), whichever order, and the per-rank shards of the global index space together give the
-    single-process budgets; blocked keeps every fused-launch group of 6 consecutive games within
-    two adjacent plies."""
+@pytest.mark.parametrize("n,L,world", [(4096, 60, 1), (16384, 32, 1), (32768, 60, 8), (1000, 60, 2),
+                                       (512, 60, 4)])
+def test_stagger_budgets_are_phase_neutral_per_rank(order, n, L, world):
+    """bench.py's stagger: within EVERY rank's shard each ply of
+    the game holds n / L games (floor or ceil), so every rank plays the same mix of phases
+    (indexing the global game space gave rank r only plies [L r / W, L (r + 1) / W)); blocked
+    keeps every fused-launch group of 6 consecutive games within two adjacent plies. The budgets
+    come from the game's index in its shard (bench.stagger: seeds - seed - first_game)."""
     import torch
     import bench
-    G = n * world
-    full = bench.stagger_budget(torch.arange(G, dtype=torch.int64), L, G, order)
-    counts = torch.bincount(full.long(), minlength=L)
-    assert counts.numel() == L and int(counts.min()) >= G // L and int(counts.max()) <= -(-G // L)
-    assert int(full.min()) >= 0 and int(full.max()) <= L - 1
-    parts = [bench.stagger_budget(torch.arange(r * n, (r + 1) * n, dtype=torch.int64), L, G, order)
-             for r in range(world)]
-    assert torch.equal(torch.cat(parts), full)
-    if order == "blocked":
-        groups = full[: G // 6 * 6].view(-1, 6)
-        assert int((groups.max(1).values - groups.min(1).values).max()) <= 1
+    seed = 42
+    for r in range(world):
+        seeds = torch.arange(r * n, (r + 1) * n, dtype=torch.int64) + seed   # the rank's lane seeds
+        bud = bench.stagger_budget(seeds - seed - r * n, L, n, order)
+        counts = torch.bincount(bud.long(), minlength=L)
+        assert counts.numel() == L and int(counts.min()) >= n // L and int(counts.max()) <= -(-n // L)
+        assert int(bud.min()) == 0 and int(bud.max()) == L - 1
+        if order == "blocked":
+            groups = bud[: n // 6 * 6].view(-1, 6)
+            assert int((groups.max(1).values - groups.min(1).values).max()) <= 1
+
+
+def test_bench_world4_dry_run_ranks_cover_every_ply():
+    """The world-4 dry run reports each rank's stagger: every rank's shard starts games at plies
+    0..59 with 8 or 9 games per ply (512 games / 60 plies) — no rank holds one phase."""
+    r = _run(["--gpus", "4", "--dist-backend", "gloo", "--dry-run", "--games", "512"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    for p in d["ranks"]["per_rank"]:
+        assert p["stagger_plies"] == [0, 59], p
+        assert p["stagger_games_per_ply"] == [8, 9], p

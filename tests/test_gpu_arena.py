@@ -3,6 +3,8 @@ import numpy as np
 import pytest
 import torch
 
+from evaluators import TableEvaluator as _TableEvaluator
+
 pytestmark = pytest.mark.gpu
 
 
@@ -42,33 +44,6 @@ def test_play_games_results_and_colours():
     r1 = arena.play_games(["net_a"] * 8 + ["random"] * 8, ["random"] * 8 + ["net_a"] * 8)
     assert len(r1) == 16 and set(r1) <= {0.0, 0.5, 1.0}
     assert arena.play_game("net_b", "net_a") in (0.0, 0.5, 1.0)
-
-
-class _TableEvaluator:
-    """A deterministic leaf evaluator with exact fp32 arithmetic on both sides (GPU torch here,
-    NumPy in the restatement): priors ((5 i + own discs) mod 8 + 1) / 16, pass 1/32, value
-    (own - opponent discs) / 64 — dyadic rationals, so the GPU and CPU searches see identical
-    NN outputs and any difference is the arena's."""
-    outputs_probs = True
-
-    def __call__(self, x):
-        own = x[:, 0].reshape(x.shape[0], -1).sum(1)
-        opp = x[:, 1].reshape(x.shape[0], -1).sum(1)
-        i = torch.arange(64, device=x.device, dtype=torch.float32)
-        p = torch.empty(x.shape[0], 65, device=x.device)
-        p[:, :64] = (torch.remainder(5 * i[None, :] + own[:, None], 8) + 1) / 16
-        p[:, 64] = 1 / 32
-        return p.contiguous(), ((own - opp) / 64).float().contiguous()
-
-    @staticmethod
-    def numpy(x):
-        own = x[:, 0].reshape(len(x), -1).sum(1).astype(np.float32)
-        opp = x[:, 1].reshape(len(x), -1).sum(1).astype(np.float32)
-        i = np.arange(64, dtype=np.float32)
-        p = np.empty((len(x), 65), np.float32)
-        p[:, :64] = (np.remainder(5 * i[None, :] + own[:, None], 8) + 1) / 16
-        p[:, 64] = 1 / 32
-        return p, ((own - opp) / 64).astype(np.float32)
 
 
 def _literal_arena_sequential(O, players, black_ids, white_ids, seed):

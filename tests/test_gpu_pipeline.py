@@ -12,7 +12,7 @@ def test_selfplay_trainer_iterations_use_the_trained_net(tmp_path):
     import rvz
     from rvz.pipeline import SelfPlayTrainer
     torch.manual_seed(0)
-    G, S = 64, 128
+    G, S = 64, 200        # four batches: distinct games (asserted below; mcts.py:96-97)
     net = rvz.AlphaZeroNetwork(8, 2, 64).cuda()
     spt = SelfPlayTrainer(net, G, num_simulations=S, seed=7, train_steps=40, train_batch=64)
     r0 = spt.run_iteration()
@@ -33,6 +33,7 @@ def test_selfplay_trainer_iterations_use_the_trained_net(tmp_path):
     assert torch.equal(t["policy_targets"], data["policy_targets"])
     assert torch.equal(t["value_targets"], data["value_targets"])
     assert sum(len(g["states"]) for g in games) == data["states"].shape[0]
+    assert len({g["states"][4].tobytes() for g in games}) > 1   # not one game in every slot
 
 
 def test_c4_shaped_iteration_over_rccl_world1(tmp_path):

@@ -92,8 +92,12 @@ def test_fused_other_geometries(board, blocks, filters, gpw):
     """The C3 trunk shape (128 filters, one board per pass; with the default queue groups and
     with bench.py's C3 groups of 16, play_group -16) and the packed 6x6 geometry (C5)."""
     net = _net(board, blocks, filters, seed=1)
-    G, S, plies = 160, 160 if board == 8 else 100, 24
-    _same(_fused(net, G, S, plies, True, True, gpw=gpw), _plain(net, G, S, plies, True, True))
+    # three (8x8) / four (6x6) leaf batches: the visits spread over two or three root children,
+    # so the games diverge (with two batches every slot plays one game, mcts.py:96-97)
+    G, S, plies = 160, 160 if board == 8 else 200, 24
+    a = _fused(net, G, S, plies, True, True, gpw=gpw)
+    assert len(set(a[1][3].tolist())) > 1                  # distinct games by the fourth ply
+    _same(a, _plain(net, G, S, plies, True, True))
 
 
 def test_fused_headline_configuration_at_full_size():
@@ -109,7 +113,7 @@ def test_fused_graph_capture_and_errors():
     call inside a pull-style search."""
     import rvz
     net = _net(8, 1, 64)
-    G, S = 64, 96
+    G, S = 64, 200        # four batches: distinct games (asserted below)
     eng = rvz.Engine(G, S, 64, memo=True)
     run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=5, fused=True)
     run.start()
@@ -121,6 +125,7 @@ def test_fused_graph_capture_and_errors():
     for x, y in zip(run.eng.get_state(), ref.eng.get_state()):
         assert torch.equal(x, y)
     assert torch.equal(run._plies, ref._plies)
+    assert len(set(run.eng.get_state()[0].tolist())) > 1   # not one game in every slot
     with pytest.raises(rvz.RvzError):
         eng.play(lambda x: net(x), 1, 1.0, run.seeds, G, run._plies, run._done)
     eng.search_begin()

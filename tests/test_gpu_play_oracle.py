@@ -266,7 +266,7 @@ def test_fused_capture_without_an_eager_ply_counts_rows():
     eager launches do."""
     import rvz
     net = _net(8, 1, 64)
-    G, S = 64, 128
+    G, S = 64, 200        # four batches: distinct games (asserted below)
     runs = []
     for graph in (True, False):
         eng = rvz.Engine(G, S, 64, memo=True)
@@ -278,8 +278,10 @@ def test_fused_capture_without_an_eager_ply_counts_rows():
         for _ in range(3):
             run.ply() if graph else run._body(2)
         torch.cuda.synchronize()
-        runs.append((int(eng.play_rows.item()), run._plies.clone()))
+        runs.append((int(eng.play_rows.item()), run._plies.clone(),
+                     eng.get_state()[0].clone()))
     assert runs[0][0] == runs[1][0] > 0 and torch.equal(runs[0][1], runs[1][1])
+    assert torch.equal(runs[0][2], runs[1][2]) and len(set(runs[0][2].tolist())) > 1
 
 
 def test_play_refuses_to_allocate_inside_a_capture(monkeypatch):

@@ -244,11 +244,13 @@ def test_large_activation_net_plays_in_selfplay(tmp_path):
     net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
     with torch.no_grad():
         net.bn.bias.fill_(1e5)
-    sp = rvz.SelfPlay(net, {"num_simulations": 128, "seed": 1, "save_dir": str(tmp_path)})
+    # 200 simulations (four batches): the games differ (asserted), so the stored images do too
+    sp = rvz.SelfPlay(net, {"num_simulations": 200, "seed": 1, "save_dir": str(tmp_path)})
     assert sp.evaluator.kernel == "h2"
     games = sp.generate_games(4)
     assert len(games) == 4 and not sp.evaluator.overflowed()
-    eng = rvz.Engine(64, 128, 64)
+    assert len({g["states"][4].tobytes() for g in games}) > 1
+    eng = rvz.Engine(64, 200, 64)
     ev = rvz.LeafEvaluator(net, kernel="h2")
     run = rvz.SelfPlayRunner(eng, ev, autoreset=True)
     run.start()
@@ -257,6 +259,7 @@ def test_large_activation_net_plays_in_selfplay(tmp_path):
     run.ply()
     run.check()
     assert not ev.overflowed()
+    assert len(set(eng.get_state()[0].tolist())) > 1
     x = torch.from_numpy(np.stack([s for g in games for s in g["states"]])).float().cuda()
     m64 = copy.deepcopy(net).double().cpu().eval()
     with torch.no_grad():
