@@ -1769,7 +1769,8 @@ static int64_t play_al4(int64_t n) { return (n + 3) / 4 * 4; }
 
 // scratch (floats): [queue words: q_next + pad, q_done[G]] (one 16-B-aligned block at the start,
 // zeroed per launch), leaf planes, need, head-conv rows, logits, value
-static int64_t play_qwords(int64_t G) { return 4 + play_al4(G); }
+// + the pass gate's words (PlayArgs::gate: 8 XCDs x 128 bytes)
+static int64_t play_qwords(int64_t G) { return 4 + play_al4(G) + 8 * 32; }
 int64_t rvz_play_scratch_size(const rvz_engine* e) {
     if (!e) return RVZ_EINVAL;
     const int64_t G = e->v.G;
@@ -1864,6 +1865,20 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.q_next = queue ? reinterpret_cast<unsigned*>(sc) : nullptr;
     pa.q_done = queue ? reinterpret_cast<unsigned*>(sc) + 4 : nullptr;
     pa.n_groups = 0;
+    // the per-XCD pass gate (rvz_play.hip.h play_gate; an experiment, off by default):
+    // RVZ_PLAY_GATE="k,us" = open a round at k arrivals or us microseconds; queue schedule only
+    // (its words are zeroed with the queue's)
+    pa.gate = queue ? reinterpret_cast<unsigned long long*>(sc + 4 + play_al4(G)) : nullptr;
+    pa.gate_k = 0;
+    pa.gate_t = 0;
+    if (const char* gs = getenv("RVZ_PLAY_GATE")) {
+        int k = 0;
+        double us = 0.0;
+        if (queue && sscanf(gs, "%d,%lf", &k, &us) == 2 && k > 0 && us > 0.0) {
+            pa.gate_k = k;
+            pa.gate_t = (unsigned)(us * 100.0);
+        }
+    }
     sc += play_qwords(G);
     pa.x = sc;
     sc += play_al4(G * 3 * e->NSQ);

@@ -60,6 +60,11 @@ struct PlayArgs {
     unsigned* q_next;
     unsigned* q_done;  // [n_groups]
     int n_groups;
+    // the per-XCD pass gate (play_gate; gate null or gate_k 0: off): [8][16] words, one 128-byte
+    // line per XCD, {round:32 | arrivals:32}, zeroed per launch with the queue words
+    unsigned long long* gate;
+    int gate_k;        // arrivals that open a round
+    unsigned gate_t;   // or this long after a waiter's arrival (s_memrealtime ticks, 100 MHz)
 };
 constexpr int PLAY_GPW_MAX = 64;
 // the 8x8 / 64-filter (C2) geometry keeps its head-conv rows in LDS for the FC heads (no
@@ -226,6 +231,43 @@ __device__ __forceinline__ int tab_insert(const PlayArgs& a, uint32_t gen, uint6
     return 0;
 }
 
+// ---- the per-XCD pass gate (an experiment on C3's weight stream, off by default) ------------
+// At 10x128 every trunk pass streams the whole 11.8 MB of f16-pair weights, and the 64 workgroups
+// of an XCD, each at its own layer, keep all of it live in a 4 MB L2 (45% L2 hits,
+// the fabric path full). The gate makes a workgroup about to start a pass wait until gate_k
+// workgroups of its XCD have arrived (or gate_t has passed), so passes start in cohorts whose
+// members then read the same layer's weights at the same time. Timing only: the games do not
+// depend on it. One lane; no data is handed over, so no fences.
+__device__ __forceinline__ void gate_open(unsigned long long* w, unsigned r) {
+    unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((unsigned)(v >> 32) == r &&
+           !__hip_atomic_compare_exchange_strong(w, &v, (unsigned long long)(r + 1u) << 32,
+                                                 __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+    }
+}
+__device__ __forceinline__ void play_gate(unsigned long long* gate, int k, unsigned t) {
+    const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // XCC_ID
+    unsigned long long* w = gate + 16 * x;
+    const unsigned long long old =
+        __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned r = (unsigned)(old >> 32);
+    if ((int)((unsigned)old + 1u) >= k) {
+        gate_open(w, r);
+        return;
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(2);
+        const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(v >> 32) != r) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > t) {
+            gate_open(w, r);
+            return;
+        }
+    }
+}
+
 struct PlayCtx {
     View v;
     PlayArgs a;
@@ -281,8 +323,11 @@ void k_play(PlayCtx ctx0) {
     // LDS: the trunk's activation image; between passes its head holds the search phase's act /
     // reset scratch (per wave) or (not HLDS) the FC heads' input rows
     constexpr int SP_BYTES = WPB * (NPOL + 7) * 8;
-    static_assert(heads_in_floats(BS) * 4 <= C::BYTES, "heads rows fit");
-    static_assert(SP_BYTES + WPB * 624 * 4 <= C::BYTES, "act / reset scratch fits");
+    // the search phase's act / reset scratch and the FC heads' rows live in the activation image
+    // only: below C::RMAX, so they never overlap the range maxima / overflow words (RangeLds),
+    // which are pass-local
+    static_assert(heads_in_floats(BS) * 4 <= C::RMAX, "heads rows fit");
+    static_assert(SP_BYTES + WPB * 624 * 4 <= C::RMAX, "act / reset scratch fits");
     __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
     __shared__ int st_k[GMAX];   // next batch of the game's search (E: act next)
     __shared__ int st_f[GMAX];   // PF_* flags
@@ -539,6 +584,16 @@ void k_play(PlayCtx ctx0) {
 
             // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
             for (int p0 = 0; p0 < nq; p0 += NBOARD) {
+                // the pass gate (off unless RVZ_PLAY_GATE; built into the 10x128 form only)
+                if constexpr (F == 128 && BS == 8) {
+                    if (play_ctx().a.gate_k > 0) {
+                        if (tid == 0) {
+                            const PlayArgs& a = play_ctx().a;
+                            play_gate(a.gate, a.gate_k, a.gate_t);
+                        }
+                        __syncthreads();
+                    }
+                }
                 const PlayArgs& a = play_ctx().a;
                 int gb[NBOARD];
 #pragma unroll

@@ -118,10 +118,12 @@ def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2, kill_after_s: float
     def on_term(signum, frame):
         raise KeyboardInterrupt(f"signal {signum}")
 
+    installed, old = False, None
     try:
         old = signal.signal(signal.SIGTERM, on_term)
+        installed = True                       # old may be None (a handler set outside Python)
     except ValueError:                         # not the main thread: no handler, finally still runs
-        old = None
+        pass
     try:
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
@@ -143,8 +145,9 @@ def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2, kill_after_s: float
         return rc
     finally:
         # a second SIGTERM during the cleanup must not raise out of it and strand live ranks
-        # (ADVICE r04): ignored until every child is gone, then the old handler is back
-        if old is not None:
+        # (ADVICE r04, r05): ignored from the first statement of the cleanup until every child is
+        # gone, then the old handler is back (SIG_DFL if it was not a Python one)
+        if installed:
             signal.signal(signal.SIGTERM, signal.SIG_IGN)
         live = [p for p in procs if p.poll() is None]
         for p in live:
@@ -156,8 +159,8 @@ def spawn_ranks(n: int, cmd: List[str], poll_s: float = 0.2, kill_after_s: float
             except subprocess.TimeoutExpired:
                 p.kill()
                 p.wait()
-        if old is not None:
-            signal.signal(signal.SIGTERM, old)
+        if installed:
+            signal.signal(signal.SIGTERM, old if old is not None else signal.SIG_DFL)
 
 
 def _device_for_backend():

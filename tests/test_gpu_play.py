@@ -195,3 +195,18 @@ def test_fused_ranged_rerun_is_per_board(board, filters):
     _same(a, (run, torch.stack(moves)))
     for r in (a[0], run):
         assert not r.evaluator.overflowed()
+
+
+@pytest.mark.parametrize("gate", ["2,20", "64,5"])
+def test_pass_gate_keeps_the_games(monkeypatch, gate):
+    """The per-XCD pass gate (RVZ_PLAY_GATE, rvz_play.hip.h play_gate; the 10x128 form's timing
+    experiment) changes when a workgroup starts a trunk pass, never what it computes: the same
+    games with the gate opened by arrivals (2 of an XCD's workgroups) and by its timeout (64
+    arrivals never come from 40 workgroups)."""
+    net = _net(8, 2, 128, seed=1)
+    G, S, plies = 160, 200, 12
+    a = _fused(net, G, S, plies, True, True, gpw=-4)
+    monkeypatch.setenv("RVZ_PLAY_GATE", gate)
+    b = _fused(net, G, S, plies, True, True, gpw=-4)
+    assert len(set(a[1][3].tolist())) > 1
+    _same(a, b)
