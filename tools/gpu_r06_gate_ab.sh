@@ -5,7 +5,7 @@
 set -u
 out=gpurun_out/r06gate
 mkdir -p "$out"
-variants=${VARIANTS:-"off 64,60 48,30 32,15"}
+variants=${VARIANTS:-"off 2,10 4,25 8,50 64,100"}
 pairs=${PAIRS:-2}
 for i in $(seq 1 "$pairs"); do
     for v in $variants; do

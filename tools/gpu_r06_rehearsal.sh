@@ -1,0 +1,25 @@
+#!/bin/bash
+# bench.py --gpus 2 / 4 rehearsals (gloo ranks sharing the one card; the
+# driver's SCALE runs use nccl = RCCL on 8 GPUs) with the rank-local stagger: every rank's
+# nn_rows_per_ply and value should agree. Output: gpurun_out/r06reh/bench_<n>rank_gloo.json.
+set -u
+out=gpurun_out/r06reh
+mkdir -p "$out"
+for n in ${RANKS:-4 2}; do
+    games=$((2048 / n))
+    timeout -k 10 400 python bench.py --gpus "$n" --dist-backend gloo --games "$games" \
+        --steps "${STEPS:-60}" --warmup 5 --no-cpu-baseline > "$out/bench_${n}rank_gloo.json" \
+        2> "$out/bench_${n}rank_gloo.err"
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "$n ranks failed rc=$rc"; exit $rc; fi
+    python - "$out/bench_${n}rank_gloo.json" <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+r = d["ranks"]
+print(d["n_gpus"], "ranks: value", d["value"], "spread",
+      {k: v["max_over_min"] for k, v in r["spread"].items()})
+for p in r["per_rank"]:
+    print("  rank", p["rank"], "value", p["value"], "rows/ply", p["nn_rows_per_ply"],
+          "table hits/ply", p.get("table_hits_per_ply"), "stagger", p.get("stagger_plies"))
+EOF
+done
