@@ -402,40 +402,6 @@ class SelfPlay:
         return passes, where
 
 
-def sequential_draw_passes(num_games: int, max_draws: int, piece: int, draws_on: bool, rng,
-                           play: Callable):
-    """Lockstep passes that give every game the piece of ONE random_sample() stream it would
-    draw if the games ran one after another (SelfPlay's class docstring; self_play.py:66-101
-    with mcts.py:684). rng: a NumPy RandomState or the np.random module (its state is read once
-    and advanced at the end by exactly the values the sequential loop draws). A game draws at
-    most max_draws values (one per move; none when draws_on is False, i.e. temperature 0,
-    mcts.py:679-681). play(U float64 [k, piece]) plays k fresh games, game j drawing U[j, 0],
-    U[j, 1], ... in order, and returns (payload, used int [k]: the values each game drew).
-    Returns (payloads of every pass, game -> (pass, index in that pass), draws per game)."""
-    G = int(num_games)
-    rs = np.random.RandomState()
-    rs.set_state(rng.get_state())
-    stream = rs.random_sample(G * max_draws + piece)
-    n = np.full(G, max_draws if draws_on else 0, np.int64)   # first guess: the longest game
-    prev: List[Optional[int]] = [None] * G
-    where: List = [None] * G
-    payloads = []
-    while True:
-        off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
-        todo = [g for g in range(G) if prev[g] != int(off[g])]
-        if not todo:
-            break
-        payload, used = play(np.stack([stream[off[g]:off[g] + piece] for g in todo]))
-        for j, g in enumerate(todo):
-            if not 0 <= int(used[j]) <= max_draws:
-                raise RuntimeError(f"game drew {int(used[j])} values (at most {max_draws})")
-            n[g], prev[g], where[g] = int(used[j]), int(off[g]), (len(payloads), j)
-        payloads.append(payload)
-    total = int(n.sum())
-    if total:                       # leave the stream where the sequential loop leaves it
-        rng.random_sample(total)
-    return payloads, where, n
-
     def _play(self, num_games: int) -> List[Dict]:
         if num_games <= 0:
             self._last_records = None
@@ -501,3 +467,38 @@ def sequential_draw_passes(num_games: int, max_draws: int, piece: int, draws_on:
         return {"states": t["states"].cpu().numpy(),
                 "action_probs": t["policy_targets"].cpu().numpy(),
                 "values": t["value_targets"].cpu().numpy()}
+
+
+def sequential_draw_passes(num_games: int, max_draws: int, piece: int, draws_on: bool, rng,
+                           play: Callable):
+    """Lockstep passes that give every game the piece of ONE random_sample() stream it would
+    draw if the games ran one after another (SelfPlay's class docstring; self_play.py:66-101
+    with mcts.py:684). rng: a NumPy RandomState or the np.random module (its state is read once
+    and advanced at the end by exactly the values the sequential loop draws). A game draws at
+    most max_draws values (one per move; none when draws_on is False, i.e. temperature 0,
+    mcts.py:679-681). play(U float64 [k, piece]) plays k fresh games, game j drawing U[j, 0],
+    U[j, 1], ... in order, and returns (payload, used int [k]: the values each game drew).
+    Returns (payloads of every pass, game -> (pass, index in that pass), draws per game)."""
+    G = int(num_games)
+    rs = np.random.RandomState()
+    rs.set_state(rng.get_state())
+    stream = rs.random_sample(G * max_draws + piece)
+    n = np.full(G, max_draws if draws_on else 0, np.int64)   # first guess: the longest game
+    prev: List[Optional[int]] = [None] * G
+    where: List = [None] * G
+    payloads = []
+    while True:
+        off = np.concatenate([[0], np.cumsum(n)[:-1]]).astype(np.int64)
+        todo = [g for g in range(G) if prev[g] != int(off[g])]
+        if not todo:
+            break
+        payload, used = play(np.stack([stream[off[g]:off[g] + piece] for g in todo]))
+        for j, g in enumerate(todo):
+            if not 0 <= int(used[j]) <= max_draws:
+                raise RuntimeError(f"game drew {int(used[j])} values (at most {max_draws})")
+            n[g], prev[g], where[g] = int(used[j]), int(off[g]), (len(payloads), j)
+        payloads.append(payload)
+    total = int(n.sum())
+    if total:                       # leave the stream where the sequential loop leaves it
+        rng.random_sample(total)
+    return payloads, where, n

@@ -113,3 +113,14 @@ def test_a_game_drawing_too_much_is_refused():
     with pytest.raises(RuntimeError, match="drew 61"):
         sequential_draw_passes(2, 60, 64, True, np.random.RandomState(0),
                                lambda U: (None, np.full(len(U), 61)))
+
+
+def test_selfplay_keeps_the_reference_interface():
+    """The drop-in class exposes the reference's methods (self_play.py:51, 161) beside the draw
+    passes (a module-level function, not part of the class body)."""
+    import inspect
+    from rvz.selfplay import SelfPlay, sequential_draw_passes
+    for name in ("generate_games", "generate_training_data", "training_tensors"):
+        assert callable(getattr(SelfPlay, name))
+    assert list(inspect.signature(SelfPlay.__init__).parameters)[:3] == ["self", "model", "args"]
+    assert inspect.isfunction(sequential_draw_passes)
