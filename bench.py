@@ -149,6 +149,10 @@ def parse(argv=None):
                          "on 8x8): blocked floor(g * L / N) (the games of a ply are consecutive, "
                          "so a game group of the fused launch plays one ply of the game), "
                          "interleaved g mod L; both put N / L games at every ply")
+    ap.add_argument("--serial-ranks", action="store_true",
+                    help="N > 1 ranks sharing one card (gloo rehearsals): the ranks take turns "
+                         "in the timed region, each with the card to itself, so the per-rank "
+                         "report compares the shards and value (sum / max) predicts N cards")
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=int, default=42)
@@ -774,17 +778,31 @@ def selfplay(args, device, rank, world, full=True):
     # launches' durations (a replay is one launch)
     ftimer = _lib.Timer(2 * n_rep) if args.fused else None
     fstream = _lib.stream_handle(device)
-    t0 = time.perf_counter()
-    t_enq = []
-    for i in range(n_rep):                 # one replay plays ppg plies
-        if ftimer is not None:
-            ftimer.record(fstream)
-        run.ply()
-        if ftimer is not None:
-            ftimer.record(fstream)
-        t_enq.append(time.perf_counter())
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
+
+    def timed():
+        torch.cuda.synchronize(device)
+        ta = time.perf_counter()
+        enq = []
+        for i in range(n_rep):                 # one replay plays ppg plies
+            if ftimer is not None:
+                ftimer.record(fstream)
+            run.ply()
+            if ftimer is not None:
+                ftimer.record(fstream)
+            enq.append(time.perf_counter())
+        torch.cuda.synchronize(device)
+        return ta, time.perf_counter(), enq
+
+    if args.serial_ranks and world > 1:
+        # rehearsal of N ranks on ONE shared card: the ranks take turns, each timing its own shard
+        # with the card to itself, so per-rank values compare shards (not the card's scheduling
+        # of N concurrent processes) and sum / max predicts N cards
+        for r in range(world):
+            rdist.barrier()
+            if r == rank:
+                t0, t1, t_enq = timed()
+    else:
+        t0, t1, t_enq = timed()
     if os.environ.get("RVZ_BENCH_ENQ"):
         iv = np.diff(np.array([t0] + t_enq)) * 1e3
         print(f"[bench] {args.config}: host enqueue ms per ply: {np.round(iv, 3).tolist()}; "
@@ -872,6 +890,9 @@ def selfplay(args, device, rank, world, full=True):
             "timed_region_trunk_frac": round(region / peak, 4),
             "timed_region_useful_frac": round(upr * rows / (t1 - t0) / 1e12 / peak, 4)}
     plies_local = s1 - s0
+    if world > 1:
+        ranks["timing"] = ("serial: the ranks took turns on a shared card (--serial-ranks)"
+                           if args.serial_ranks else "concurrent")
     out = {"value": value, "dt": dt, "total": total, "roofline": roof, "net": net, "ranks": ranks,
            "eng": eng, "ev": ev, "lanes": args.lanes,
            "nn_rows_per_ply": round(rows / max(1, plies_local), 3),

