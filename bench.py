@@ -712,6 +712,16 @@ def selfplay(args, device, rank, world, full=True):
                                          fused_bookkeeping=not args.torch_bookkeeping)
         engines = [run.eng]
     eng, ev = lane0.eng, lane0.evaluator    # instrumentation: one lane's kernels
+    # --serial-ranks (N ranks rehearsed on ONE shared card): the ranks take turns from here to the
+    # end of the timed region, each with the card to itself (stagger, warm-up and timed plies:
+    # four persistent fused launches of 512 workgroups each on one card would time-slice and trip
+    # the task queue's bounded wait), so the per-rank values compare the shards and sum / max
+    # predicts N cards. Rank r waits for rounds 0..r-1 (ranks 0..r-1 done), runs, then joins the
+    # remaining rounds: `world` barrier calls per rank in all.
+    serial = args.serial_ranks and world > 1
+    if serial:
+        for _ in range(rank):
+            rdist.barrier()
     run.start()
     tag = "" if getattr(args, "label", None) is None else args.label + "."
     stagger_plies = 0.0
@@ -770,7 +780,8 @@ def selfplay(args, device, rank, world, full=True):
     tab0 = eng.table_stats.clone() if args.fused else None
     if graph_events:
         graph_events[1].zero_()            # the ring starts with the timed region
-    rdist.barrier()
+    if not serial:
+        rdist.barrier()
     torch.cuda.synchronize(device)
     s0 = int(run.steps.item())
     n_rep = args.steps // ppg
@@ -793,21 +804,16 @@ def selfplay(args, device, rank, world, full=True):
         torch.cuda.synchronize(device)
         return ta, time.perf_counter(), enq
 
-    if args.serial_ranks and world > 1:
-        # rehearsal of N ranks on ONE shared card: the ranks take turns, each timing its own shard
-        # with the card to itself, so per-rank values compare shards (not the card's scheduling
-        # of N concurrent processes) and sum / max predicts N cards
-        for r in range(world):
-            rdist.barrier()
-            if r == rank:
-                t0, t1, t_enq = timed()
-    else:
-        t0, t1, t_enq = timed()
+    t0, t1, t_enq = timed()
     if os.environ.get("RVZ_BENCH_ENQ"):
         iv = np.diff(np.array([t0] + t_enq)) * 1e3
         print(f"[bench] {args.config}: host enqueue ms per ply: {np.round(iv, 3).tolist()}; "
               f"device total {(t1 - t0) * 1e3:.1f} ms", file=sys.stderr)
-    rdist.barrier()
+    if serial:
+        for _ in range(world - rank):      # this rank's turn is over; the later ranks' turns
+            rdist.barrier()
+    else:
+        rdist.barrier()
     s1 = int(run.steps.item())
     rows1 = rows_now()
     tab_d = (eng.table_stats - tab0).tolist() if tab0 is not None else None

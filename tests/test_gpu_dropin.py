@@ -7,7 +7,7 @@ import golden_replay as R
 
 pytestmark = pytest.mark.gpu
 
-SEED_H2_800 = 0        # placeholder until the MI355X scan (see DRAW_ORDER_CASE)
+SEED_H2_800 = 727      # game 7 of 12 ends after 34 moves, games 2 and 3 hold passes
 
 
 class _Recorder:
