@@ -1866,17 +1866,20 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.q_done = queue ? reinterpret_cast<unsigned*>(sc) + 4 : nullptr;
     pa.n_groups = 0;
     // the per-XCD pass gate (rvz_play.hip.h play_gate; an experiment, off by default):
-    // RVZ_PLAY_GATE="k,us" = open a round at k arrivals or us microseconds; queue schedule only
+    // RVZ_PLAY_GATE="k,us[,late_us]" = open a round at k arrivals or us microseconds (a
+    // workgroup arriving within late_us of a round's opening joins it at once); queue schedule only
     // (its words are zeroed with the queue's)
     pa.gate = queue ? reinterpret_cast<unsigned long long*>(sc + 4 + play_al4(G)) : nullptr;
     pa.gate_k = 0;
     pa.gate_t = 0;
-    if (const char* gs = getenv("RVZ_PLAY_GATE")) {
+    pa.gate_late = 0;
+    if (const char* gs = getenv("RVZ_PLAY_GATE")) {   // "k,us[,late_us]"
         int k = 0;
-        double us = 0.0;
-        if (queue && sscanf(gs, "%d,%lf", &k, &us) == 2 && k > 0 && us > 0.0) {
+        double us = 0.0, late = 0.0;
+        if (queue && sscanf(gs, "%d,%lf,%lf", &k, &us, &late) >= 2 && k > 0 && us > 0.0) {
             pa.gate_k = k;
             pa.gate_t = (unsigned)(us * 100.0);
+            pa.gate_late = late > 0.0 ? (unsigned)(late * 100.0) : 0u;
         }
     }
     sc += play_qwords(G);

@@ -65,6 +65,7 @@ struct PlayArgs {
     unsigned long long* gate;
     int gate_k;        // arrivals that open a round
     unsigned gate_t;   // or this long after a waiter's arrival (s_memrealtime ticks, 100 MHz)
+    unsigned gate_late;  // a workgroup arriving this soon after a round opened joins it at once
 };
 constexpr int PLAY_GPW_MAX = 64;
 // the 8x8 / 64-filter (C2) geometry keeps its head-conv rows in LDS for the FC heads (no
@@ -238,17 +239,28 @@ __device__ __forceinline__ int tab_insert(const PlayArgs& a, uint32_t gen, uint6
 // workgroups of its XCD have arrived (or gate_t has passed), so passes start in cohorts whose
 // members then read the same layer's weights at the same time. Timing only: the games do not
 // depend on it. One lane; no data is handed over, so no fences.
+// word 0 of an XCD's line: {round:32 | arrivals:32}; word 1: when the current round opened
 __device__ __forceinline__ void gate_open(unsigned long long* w, unsigned r) {
     unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while ((unsigned)(v >> 32) == r &&
-           !__hip_atomic_compare_exchange_strong(w, &v, (unsigned long long)(r + 1u) << 32,
+    while ((unsigned)(v >> 32) == r) {
+        if (__hip_atomic_compare_exchange_strong(w, &v, (unsigned long long)(r + 1u) << 32,
                                                  __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(w + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
     }
 }
-__device__ __forceinline__ void play_gate(unsigned long long* gate, int k, unsigned t) {
+__device__ __forceinline__ void play_gate(unsigned long long* gate, int k, unsigned t,
+                                          unsigned late) {
     const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // XCC_ID
     unsigned long long* w = gate + 16 * x;
+    if (late) {   // the round that opened moments ago: join its cohort without an arrival
+        const unsigned long long t_open =
+            __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t_open && __builtin_amdgcn_s_memrealtime() - t_open < late) return;
+    }
     const unsigned long long old =
         __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned r = (unsigned)(old >> 32);
@@ -589,7 +601,7 @@ void k_play(PlayCtx ctx0) {
                     if (play_ctx().a.gate_k > 0) {
                         if (tid == 0) {
                             const PlayArgs& a = play_ctx().a;
-                            play_gate(a.gate, a.gate_k, a.gate_t);
+                            play_gate(a.gate, a.gate_k, a.gate_t, a.gate_late);
                         }
                         __syncthreads();
                     }

@@ -197,7 +197,7 @@ def test_fused_ranged_rerun_is_per_board(board, filters):
         assert not r.evaluator.overflowed()
 
 
-@pytest.mark.parametrize("gate", ["2,20", "64,5"])
+@pytest.mark.parametrize("gate", ["2,20", "64,5", "4,20,10"])
 def test_pass_gate_keeps_the_games(monkeypatch, gate):
     """The per-XCD pass gate (RVZ_PLAY_GATE, rvz_play.hip.h play_gate; the 10x128 form's timing
     experiment) changes when a workgroup starts a trunk pass, never what it computes: the same
