@@ -1093,6 +1093,8 @@ struct rvz_engine {
     int64_t tslots = 0;
     int tmaxd = 0;
     const void* tab_blob = nullptr;   // the weight blob the current generation's rows came from
+    // rvz_play_gate: the per-XCD pass gate of the 10x128 k_play form (fraction < 0: the default)
+    double gate_frac = -1.0, gate_us = 0.0, gate_late_us = 0.0;
 };
 
 static thread_local std::string g_create_error;
@@ -1611,6 +1613,18 @@ int rvz_search_memo_reset(rvz_engine* e) {
     return r != RVZ_OK ? r : table_bump(e);   // new weights: the table's rows are stale too
 }
 
+int rvz_play_gate(rvz_engine* e, double fraction, double timeout_us, double late_us) {
+    if (!e || !(fraction <= 1.0) || !(timeout_us >= 0.0) || !(late_us >= 0.0) ||
+        timeout_us > 1e6 || late_us > 1e6) {
+        if (e) e->err = "rvz_play_gate: fraction <= 1 (< 0: the default), 0 <= us <= 1e6";
+        return RVZ_EINVAL;
+    }
+    e->gate_frac = fraction;
+    e->gate_us = timeout_us;
+    e->gate_late_us = late_us;
+    return RVZ_OK;
+}
+
 int rvz_play_table(rvz_engine* e, int64_t slots, int32_t max_discs) {
     if (!e) return RVZ_EINVAL;
     if (slots != 0 && (slots < 1024 || (slots & (slots - 1)) != 0 || slots > (1ll << 30) ||
@@ -1781,6 +1795,18 @@ int64_t rvz_play_scratch_size(const rvz_engine* e) {
 #ifndef RVZ_PLAY_GROUP
 #define RVZ_PLAY_GROUP 4      // games per task of the queue schedule
 #endif
+// the pass gate's default (rvz_play_gate; measured on C3, profiles/r06c_gate_ab_*): a round opens
+// when 0.8 of the XCD's running workgroups arrived or 400 us after a waiter's arrival; a workgroup
+// arriving within 200 us of a round's opening joins it at once
+#ifndef RVZ_PLAY_GATE_FRAC
+#define RVZ_PLAY_GATE_FRAC 0.8
+#endif
+#ifndef RVZ_PLAY_GATE_US
+#define RVZ_PLAY_GATE_US 400.0
+#endif
+#ifndef RVZ_PLAY_GATE_LATE_US
+#define RVZ_PLAY_GATE_LATE_US 200.0
+#endif
 extern "C++" {
 template <int F, int NB, int CTW, int PTW, int BS, int OCC>
 static int play_launch(rvz_engine* e, const View& v, const PlayArgs& pa, int slots_per_cu) {
@@ -1865,22 +1891,27 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.q_next = queue ? reinterpret_cast<unsigned*>(sc) : nullptr;
     pa.q_done = queue ? reinterpret_cast<unsigned*>(sc) + 4 : nullptr;
     pa.n_groups = 0;
-    // the per-XCD pass gate (rvz_play.hip.h play_gate; an experiment, off by default):
-    // RVZ_PLAY_GATE="k,us[,late_us]" = open a round at k arrivals or us microseconds (a
-    // workgroup arriving within late_us of a round's opening joins it at once); queue schedule only
-    // (its words are zeroed with the queue's)
+    // the per-XCD pass gate (rvz_play.hip.h play_gate, rvz_play_gate; the 10x128 form only, queue
+    // schedule only: its words are zeroed with the queue's)
     pa.gate = queue ? reinterpret_cast<unsigned long long*>(sc + 4 + play_al4(G)) : nullptr;
-    pa.gate_k = 0;
-    pa.gate_t = 0;
-    pa.gate_late = 0;
-    if (const char* gs = getenv("RVZ_PLAY_GATE")) {   // "k,us[,late_us]"
-        int k = 0;
-        double us = 0.0, late = 0.0;
-        if (queue && sscanf(gs, "%d,%lf,%lf", &k, &us, &late) >= 2 && k > 0 && us > 0.0) {
-            pa.gate_k = k;
-            pa.gate_t = (unsigned)(us * 100.0);
-            pa.gate_late = late > 0.0 ? (unsigned)(late * 100.0) : 0u;
+    {   // rvz_play_gate's setting (default: RVZ_PLAY_GATE_DEFAULT), RVZ_PLAY_GATE overriding it
+        double frac = e->gate_frac, us = e->gate_us, late = e->gate_late_us;
+        if (frac < 0.0) {
+            frac = RVZ_PLAY_GATE_FRAC;
+            us = RVZ_PLAY_GATE_US;
+            late = RVZ_PLAY_GATE_LATE_US;
         }
+        if (const char* gs = getenv("RVZ_PLAY_GATE")) {   // "fraction,us[,late_us]" or "off"
+            double f = 0.0, u = 0.0, l = 0.0;
+            const int n = sscanf(gs, "%lf,%lf,%lf", &f, &u, &l);
+            frac = n >= 2 ? f : 0.0;
+            us = u;
+            late = n >= 3 ? l : 0.0;
+        }
+        pa.gate_frac = (queue && frac > 0.0 && us > 0.0)
+                           ? (unsigned)(fmin(frac, 1.0) * 65536.0 + 0.5) : 0u;
+        pa.gate_t = (unsigned)(us * 100.0);
+        pa.gate_late = late > 0.0 ? (unsigned)(late * 100.0) : 0u;
     }
     sc += play_qwords(G);
     pa.x = sc;

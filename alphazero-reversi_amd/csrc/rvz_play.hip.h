@@ -60,11 +60,12 @@ struct PlayArgs {
     unsigned* q_next;
     unsigned* q_done;  // [n_groups]
     int n_groups;
-    // the per-XCD pass gate (play_gate; gate null or gate_k 0: off): [8][16] words, one 128-byte
-    // line per XCD, {round:32 | arrivals:32}, zeroed per launch with the queue words
+    // the per-XCD pass gate (play_gate; gate null or gate_frac 0: off): [8][16] words, one
+    // 128-byte line per XCD, zeroed per launch with the queue words
     unsigned long long* gate;
-    int gate_k;        // arrivals that open a round
-    unsigned gate_t;   // or this long after a waiter's arrival (s_memrealtime ticks, 100 MHz)
+    unsigned gate_frac;  // a round opens when this fraction (Q16) of the XCD's running workgroups
+                         // arrived,
+    unsigned gate_t;     // or this long after a waiter's arrival (s_memrealtime ticks, 100 MHz);
     unsigned gate_late;  // a workgroup arriving this soon after a round opened joins it at once
 };
 constexpr int PLAY_GPW_MAX = 64;
@@ -232,14 +233,17 @@ __device__ __forceinline__ int tab_insert(const PlayArgs& a, uint32_t gen, uint6
     return 0;
 }
 
-// ---- the per-XCD pass gate (an experiment on C3's weight stream, off by default) ------------
+// ---- the per-XCD pass gate (rvz_play_gate; the 10x128 form) ---------------------------------
 // At 10x128 every trunk pass streams the whole 11.8 MB of f16-pair weights, and the 64 workgroups
 // of an XCD, each at its own layer, keep all of it live in a 4 MB L2 (45% L2 hits,
-// the fabric path full). The gate makes a workgroup about to start a pass wait until gate_k
-// workgroups of its XCD have arrived (or gate_t has passed), so passes start in cohorts whose
-// members then read the same layer's weights at the same time. Timing only: the games do not
-// depend on it. One lane; no data is handed over, so no fences.
-// word 0 of an XCD's line: {round:32 | arrivals:32}; word 1: when the current round opened
+// the fabric path full, the clock held at 1.55 GHz). The gate makes a workgroup about to start a
+// pass wait until a fraction of its XCD's running workgroups have arrived (or a timeout), so the
+// XCD's passes start in one cohort whose members read the same layer's weights at the same time;
+// a workgroup arriving shortly after a round opened (a search phase made it late) joins that
+// cohort at once instead of waiting for the next. Timing only: the games do not depend on it. One
+// lane; no data is handed over, so no fences.
+// An XCD's line: word 0 {round:32 | arrivals:32}, word 1 when the current round opened
+// (s_memrealtime), word 2 the XCD's running workgroups of this launch.
 __device__ __forceinline__ void gate_open(unsigned long long* w, unsigned r) {
     unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while ((unsigned)(v >> 32) == r) {
@@ -252,19 +256,30 @@ __device__ __forceinline__ void gate_open(unsigned long long* w, unsigned r) {
         }
     }
 }
-__device__ __forceinline__ void play_gate(unsigned long long* gate, int k, unsigned t,
-                                          unsigned late) {
+__device__ __forceinline__ unsigned long long* gate_line(unsigned long long* gate) {
     const unsigned x = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // XCC_ID
-    unsigned long long* w = gate + 16 * x;
+    return gate + 16 * x;
+}
+// a workgroup starts (+1) / ends (-1) its part of the launch on this XCD
+__device__ __forceinline__ void gate_running(unsigned long long* gate, long long d) {
+    __hip_atomic_fetch_add(gate_line(gate) + 2, (unsigned long long)d, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void play_gate(unsigned long long* gate, unsigned frac, unsigned t,
+                                          unsigned late) {
+    unsigned long long* w = gate_line(gate);
     if (late) {   // the round that opened moments ago: join its cohort without an arrival
         const unsigned long long t_open =
             __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (t_open && __builtin_amdgcn_s_memrealtime() - t_open < late) return;
     }
+    const unsigned long long running =
+        __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = max(1u, (unsigned)((running * frac) >> 16));
     const unsigned long long old =
         __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned r = (unsigned)(old >> 32);
-    if ((int)((unsigned)old + 1u) >= k) {
+    if ((unsigned)old + 1u >= k) {
         gate_open(w, r);
         return;
     }
@@ -374,6 +389,10 @@ void k_play(PlayCtx ctx0) {
     }
     double* sp = reinterpret_cast<double*>(smem) + wave * (NPOL + 7);
     uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
+    if constexpr (F == 128 && BS == 8) {   // the pass gate counts the XCD's running workgroups
+        const PlayArgs& a = play_ctx().a;
+        if (tid == 0 && a.gate_frac > 0) gate_running(a.gate, 1);
+    }
     PT_NOW(t_start);
     for (int task_i = 0;; ++task_i) {
         // ---- the next task: a game group and the ply it starts at
@@ -598,10 +617,10 @@ void k_play(PlayCtx ctx0) {
             for (int p0 = 0; p0 < nq; p0 += NBOARD) {
                 // the pass gate (off unless RVZ_PLAY_GATE; built into the 10x128 form only)
                 if constexpr (F == 128 && BS == 8) {
-                    if (play_ctx().a.gate_k > 0) {
+                    if (play_ctx().a.gate_frac > 0) {
                         if (tid == 0) {
                             const PlayArgs& a = play_ctx().a;
-                            play_gate(a.gate, a.gate_k, a.gate_t, a.gate_late);
+                            play_gate(a.gate, a.gate_frac, a.gate_t, a.gate_late);
                         }
                         __syncthreads();
                     }
@@ -665,6 +684,10 @@ void k_play(PlayCtx ctx0) {
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+    }
+    if constexpr (F == 128 && BS == 8) {   // no more passes from this workgroup
+        const PlayArgs& a = play_ctx().a;
+        if (tid == 0 && a.gate_frac > 0) gate_running(a.gate, -1);
     }
 #ifdef RVZ_PLAY_TIMING
     {

@@ -79,6 +79,7 @@ SIGNATURES = {
     "rvz_play_scratch_size": (C.c_int64, [_P]),
     "rvz_play": (C.c_int, [_P, _P]),
     "rvz_play_table": (C.c_int, [_P, C.c_int64, C.c_int32]),
+    "rvz_play_gate": (C.c_int, [_P, C.c_double, C.c_double, C.c_double]),
     "rvz_counters": (C.c_int, [_P, C.POINTER(C.c_int64)]),
     "rvz_stats_enable": (C.c_int, [_P, C.c_int32]),
     "rvz_stats_read": (C.c_int, [_P, C.POINTER(C.c_int64)]),

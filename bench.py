@@ -124,6 +124,10 @@ def parse(argv=None):
                          "(the preset decides by default: C2 and C5 fused, C1/C3/C4 not)")
     ap.add_argument("--no-fused", dest="fused", action="store_false",
                     help="the pull-style per-batch launches (k_step / trunk / heads per lane)")
+    ap.add_argument("--play-gate", default="default",
+                    help="--fused at 10x128: the per-XCD pass gate (rvz_play_gate): 'default' "
+                         "(0.8 of an XCD's running workgroups / 400 us / late join 200 us), 'off', "
+                         "or 'fraction,us,late_us'")
     ap.add_argument("--play-group", type=int, default=None,
                     help="--fused: rvz_play games_per_workgroup (> 0 static ownership; <= 0 the "
                          "task queue with groups of -N games, 0 the default)")
@@ -409,6 +413,16 @@ def stagger(args, runners, tag, device, first_game=0):
     return tot / max(1, n)
 
 
+def play_gate_setting(text):
+    """--play-gate 'off' | 'fraction,us,late_us' -> rvz_play_gate's arguments."""
+    if text == "off":
+        return (0.0, 0.0, 0.0)
+    vals = [float(v) for v in text.split(",")]
+    if len(vals) != 3:
+        raise SystemExit("--play-gate: 'default', 'off' or 'fraction,us,late_us'")
+    return tuple(vals)
+
+
 def make_net(args, device):
     import rvz
     torch.manual_seed(0)
@@ -682,6 +696,8 @@ def selfplay(args, device, rank, world, full=True):
                        compact_leaves=not args.no_compact, memo=not args.no_memo)
         if args.table and args.fused:      # the table serves rvz_play (the fused launch) only
             e.table(args.table_slots, args.table_discs)
+        if args.fused and args.play_gate != "default":
+            e.play_gate(*play_gate_setting(args.play_gate))
         return e
 
     first_game = rank * args.games          # global game index space: rank r owns a shard
@@ -912,6 +928,8 @@ def selfplay(args, device, rank, world, full=True):
            "host_enqueue_ms_per_step": round((t_enq[-1] - t0) / max(1, args.steps) * 1e3, 3),
            "plies_per_graph": ppg,
            "play_group": args.play_group if args.fused else None,
+           "play_gate": (args.play_gate if args.fused and args.filters == 128 and args.board == 8
+                         else None),
            "warmup_plies": {"stagger_mean": round(stagger_plies, 2),
                             "stagger": None if args.no_stagger else
                             f"game g of N at ply " + (
@@ -971,7 +989,8 @@ def sub_config(base, name, device, rank, world):
                        f"ResNet, {a.board}x{a.board}, {a.lanes} lane(s)",
            "games_per_gpu": a.games, "sims": a.sims, "nn": f"{a.blocks}x{a.filters}",
            "board": a.board, "lanes": a.lanes, "nn_rows_per_ply": r["nn_rows_per_ply"],
-           "warmup_plies": r["warmup_plies"], "table": r["table"], "roofline": r["roofline"]}
+           "warmup_plies": r["warmup_plies"], "table": r["table"], "roofline": r["roofline"],
+           "play_gate": r.get("play_gate")}
     del r
     torch.cuda.empty_cache()
     return out

@@ -30,9 +30,11 @@ def _plain(net, G, S, plies, memo, skip, seed_base=42):
     return run, torch.stack(moves)
 
 
-def _fused(net, G, S, plies, memo, skip, seed_base=42, gpw=0, chunks=(None,)):
+def _fused(net, G, S, plies, memo, skip, seed_base=42, gpw=0, chunks=(None,), gate=None):
     import rvz
     eng = rvz.Engine(G, S, 64, board_size=net.board_size, memo=memo)
+    if gate is not None:                  # rvz_play_gate (fraction, us, late_us); default: on
+        eng.play_gate(*gate)
     run = rvz.SelfPlayRunner(eng, rvz.LeafEvaluator(net), autoreset=True, seed_base=seed_base,
                              skip_last_eval=skip, fused=True)
     run.start()
@@ -197,16 +199,26 @@ def test_fused_ranged_rerun_is_per_board(board, filters):
         assert not r.evaluator.overflowed()
 
 
-@pytest.mark.parametrize("gate", ["2,20", "64,5", "4,20,10"])
-def test_pass_gate_keeps_the_games(monkeypatch, gate):
-    """The per-XCD pass gate (RVZ_PLAY_GATE, rvz_play.hip.h play_gate; the 10x128 form's timing
-    experiment) changes when a workgroup starts a trunk pass, never what it computes: the same
-    games with the gate opened by arrivals (2 of an XCD's workgroups) and by its timeout (64
-    arrivals never come from 40 workgroups)."""
+@pytest.mark.parametrize("gate", [(-1.0, 0.0, 0.0), (0.05, 20.0, 0.0), (1.0, 5.0, 0.0),
+                                  (0.5, 20.0, 10.0)], ids=["default", "low", "timeout", "late"])
+def test_pass_gate_keeps_the_games(gate):
+    """The per-XCD pass gate (rvz_play_gate, rvz_play.hip.h play_gate; the 10x128 form) changes
+    when a workgroup starts a trunk pass, never what it computes: the same games with the gate
+    off and with the default setting (on), rounds opened by a low arrival fraction, by the timeout
+    (every running workgroup of an XCD never arrives together), and with the late-join window."""
     net = _net(8, 2, 128, seed=1)
     G, S, plies = 160, 200, 12
-    a = _fused(net, G, S, plies, True, True, gpw=-4)
-    monkeypatch.setenv("RVZ_PLAY_GATE", gate)
-    b = _fused(net, G, S, plies, True, True, gpw=-4)
+    a = _fused(net, G, S, plies, True, True, gpw=-4, gate=(0.0, 0.0, 0.0))
+    b = _fused(net, G, S, plies, True, True, gpw=-4, gate=gate)
     assert len(set(a[1][3].tolist())) > 1
     _same(a, b)
+
+
+def test_pass_gate_setting_is_checked():
+    import rvz
+    eng = rvz.Engine(8, 64, 64)
+    for bad in ((1.5, 10.0, 0.0), (0.5, -1.0, 0.0), (0.5, 10.0, -1.0), (0.5, 2e6, 0.0)):
+        with pytest.raises(rvz.RvzError, match="rvz_play_gate"):
+            eng.play_gate(*bad)
+    eng.play_gate(0.0)                    # off
+    eng.play_gate()                       # the default
