@@ -9,8 +9,7 @@ variants=${VARIANTS:-"off 2,10 4,25 8,50 64,100"}
 pairs=${PAIRS:-2}
 for i in $(seq 1 "$pairs"); do
     for v in $variants; do
-        gate="$v"
-        [ "$v" = off ] && gate=""     # unparsable: the gate stays off
+        gate="$v"     # RVZ_PLAY_GATE: "fraction,us,late_us" (round 6 first form: "k,us[,late]"), "off"
         RVZ_PLAY_GATE="$gate" timeout -k 10 240 python bench.py --config c3 --steps 20 \
             --warmup 1 --no-cpu-baseline --sub-configs none > "$out/$v.$i.json" 2> "$out/$v.$i.err"
         rc=$?

@@ -1,13 +1,14 @@
 #!/bin/bash
 # Round 6, VERDICT r05 item 4(b): what the per-XCD pass gate does to C3's caches and clock.
 # tools/exp_c3_clock.py fused (k_play in bench's C3 form: stagger, then 2 x 20-ply launches) with
-# RVZ_PLAY_GATE unset and set, one plain run each, then one rocprofv3 --pmc pass per counter group
+# the gate off and at its default (or GATES="off f,us,late ..."), one plain run each, then one rocprofv3 --pmc pass per counter group
 # (kernel trace only). Averages over the last 2 k_play dispatches (the 20-ply launches).
 set -u
 OUT=${OUT:-gpurun_out/r06pmc}; mkdir -p "$OUT"; export TMPDIR=/tmp
-GATES=${GATES:-"off 56,100"}
+GATES=${GATES:-"off default"}
 for g in $GATES; do
-  if [ "$g" = off ]; then unset RVZ_PLAY_GATE; else export RVZ_PLAY_GATE="$g"; fi
+  # RVZ_PLAY_GATE="fraction,us,late_us" or "off"; default: the engine's setting (rvz_play_gate)
+  if [ "$g" = default ]; then unset RVZ_PLAY_GATE; else export RVZ_PLAY_GATE="$g"; fi
   tag=${g/,/_}
   timeout -k 10 240 python tools/exp_c3_clock.py fused > "$OUT/plain_$tag.json" 2> "$OUT/plain_$tag.err"
   rc=$?; echo "plain $g rc=$rc"; [ $rc -ne 0 ] && exit $rc
