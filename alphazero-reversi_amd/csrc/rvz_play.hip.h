@@ -275,6 +275,9 @@ __device__ __forceinline__ void play_gate(unsigned long long* gate, unsigned fra
     }
     const unsigned long long running =
         __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a few workgroups per XCD (a small launch, or a launch's tail) share the L2 without help:
+    // no cohort to wait for
+    if (running < 4) return;
     const unsigned k = max(1u, (unsigned)((running * frac) >> 16));
     const unsigned long long old =
         __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
