@@ -255,9 +255,12 @@ def test_gpu_trainer_tracks_the_reference_train_epoch_restatement():
     (tests/test_trainer_cpu.py::_reference_train_epoch, pipeline.py:272-366, bitwise equal to
     DDPTrainer on the CPU): same init, data and batch order (the DataLoader's seeded permutation),
     two epochs with the MultiStepLR step between them. The GPU's convolutions round differently
-    from the CPU's, so the check is fp32-class: each epoch's averaged losses within 1e-5
-    relative, every parameter within 2e-5 of its CPU value (the parameters move by ~1e-3 over
-    the 8 AdamW steps); the measured gaps go to gpurun_out/trainer_gpu_vs_cpu.json."""
+    from the CPU's, so the check is fp32-class against a float64 run of the same algorithm
+    (DDPTrainer on the CPU in float64): each epoch's averaged losses within 1e-5 relative of the
+    CPU restatement's, and the GPU's parameters no further from the float64 ones than 8x the CPU
+    float32 restatement's distance (AdamW divides by sqrt(v), so near-zero gradients turn
+    rounding into visible parameter differences on either device). Measured gaps:
+    gpurun_out/trainer_gpu_vs_cpu.json."""
     import copy
     import json
     import os
@@ -267,29 +270,35 @@ def test_gpu_trainer_tracks_the_reference_train_epoch_restatement():
     torch.manual_seed(0)
     cpu_net = rvz.AlphaZeroNetwork(8, 2, 64)
     gpu_net = copy.deepcopy(cpu_net).cuda()
+    f64_net = copy.deepcopy(cpu_net).double()
     init = {k: v.clone() for k, v in cpu_net.state_dict().items()}
     data = _data(n=200, seed=3)
     tr = DDPTrainer(gpu_net, lr_milestones=[1], lr_gamma=0.1)
+    t64 = DDPTrainer(f64_net, lr_milestones=[1], lr_gamma=0.1)
     opt = torch.optim.AdamW(cpu_net.parameters(), lr=1e-3, weight_decay=1e-4)
     sched = torch.optim.lr_scheduler.MultiStepLR(opt, milestones=[1], gamma=0.1)
     gdata = {k: v.cuda() for k, v in data.items()}
-    rep = {"loss_rel": [], "param_max_abs": None, "moved_max_abs": None}
+    ddata = {k: v.double() for k, v in data.items()}
+    rep = {"loss_rel": []}
     for ep in range(2):
         got = tr.train_epoch(gdata, seed=10 + ep)
         tr.scheduler_step()
+        t64.train_epoch(ddata, seed=10 + ep)
+        t64.scheduler_step()
         want = _reference_train_epoch(cpu_net, opt, data, 64, torch.Generator().manual_seed(10 + ep))
         sched.step()
         assert got["steps"] == 4 and got["train/lr"] == want["train/lr"]
-        rel = max(abs(got[k] - want[k]) / max(1e-12, abs(want[k]))
-                  for k in ("train/loss", "train/policy_loss", "train/value_loss"))
-        rep["loss_rel"].append(rel)
-    sg, sc = gpu_net.state_dict(), cpu_net.state_dict()
-    diffs = {k: (sg[k].detach().cpu().double() - sc[k].double()).abs().max().item()
-             for k in sc if sc[k].is_floating_point() and "running" not in k}
-    moved = max((sc[k].double() - init[k].double()).abs().max().item()
-                for k in sc if sc[k].is_floating_point() and "running" not in k)
-    rep["param_max_abs"], rep["moved_max_abs"] = max(diffs.values()), moved
-    rep["worst_param"] = max(diffs, key=diffs.get)
+        rep["loss_rel"].append(max(abs(got[k] - want[k]) / max(1e-12, abs(want[k]))
+                                   for k in ("train/loss", "train/policy_loss",
+                                             "train/value_loss")))
+    sg, sc, sd = gpu_net.state_dict(), cpu_net.state_dict(), f64_net.state_dict()
+    keys = [k for k in sc if sc[k].is_floating_point() and "running" not in k]
+
+    def dist(a):
+        return max((a[k].detach().cpu().double() - sd[k].double()).abs().max().item() for k in keys)
+
+    rep["gpu_vs_f64"], rep["cpu_vs_f64"] = dist(sg), dist(sc)
+    rep["moved_max_abs"] = max((sc[k].double() - init[k].double()).abs().max().item() for k in keys)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     try:
         os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
@@ -299,4 +308,5 @@ def test_gpu_trainer_tracks_the_reference_train_epoch_restatement():
         pass
     print(rep)
     assert max(rep["loss_rel"]) <= 1e-5, rep
-    assert rep["param_max_abs"] <= 2e-5 and moved > 1e-4, rep
+    assert rep["moved_max_abs"] > 1e-3, rep
+    assert rep["gpu_vs_f64"] <= 8 * rep["cpu_vs_f64"] + 1e-6, rep
