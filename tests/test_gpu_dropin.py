@@ -128,7 +128,7 @@ def test_selfplay_reference_draw_order(oracle, tmp_path, kind):
     seed, sims = DRAW_ORDER_CASE[kind]
     n = 12
     sp = rvz.SelfPlay(net, {"num_simulations": sims, "save_dir": str(tmp_path),
-                            "fused": kind == "h2-fused"},
+                            "fused": kind == "h2-fused"},   # h2: the pull-style loop
                       evaluator=TableEvaluator() if kind == "table" else None)
     np.random.seed(seed)
     got = sp.generate_games(n)
@@ -204,6 +204,7 @@ def test_selfplay_dropin_compaction_is_exact(tmp_path):
     out = []
     for compact in (True, False):
         sp = rvz.SelfPlay(net, {"num_simulations": 128, "seed": 5, "compact_leaves": compact,
+                                "fused": False,        # compaction is the pull-style loop's
                                 "save_dir": str(tmp_path / str(compact))})
         assert sp.evaluator.accepts_live_count
         out.append(sp.generate_games(16))
