@@ -15,7 +15,8 @@ from .engine import (Engine, board_apply, board_canonical, board_legal,  # noqa:
                      policy_softmax)
 from .game import Board, ReversiGame  # noqa: F401
 from .mcts import MCTS  # noqa: F401
-from .network import AlphaZeroNetwork, LeafEvaluator, load_reference_state_dict  # noqa: F401
+from .network import (AlphaZeroNetwork, LeafEvaluator, ModuleEvaluator,  # noqa: F401
+                      load_reference_state_dict)
 from .selfplay import LaneRunner, SelfPlay, SelfPlayRunner  # noqa: F401
 
 __version__ = "0.1.0"

@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from .engine import Engine
-from .network import LeafEvaluator
+from .network import leaf_evaluator
 
 
 class ELORatingSystem:
@@ -99,7 +99,7 @@ class ELOPlayer:
 
     def __init__(self, player_id: str, model=None, mcts_params: Optional[Dict] = None,
                  device: str = "cuda", nn_dtype=torch.float32, evaluator=None):
-        """evaluator: the leaf evaluator of a model player (default LeafEvaluator(model), the h2
+        """evaluator: the leaf evaluator of a model player (default leaf_evaluator(model): the h2
         kernels); any callable leaf_x -> (logits, value) works (``outputs_probs = True``:
         softmaxed rows)."""
         self.player_id = player_id
@@ -114,7 +114,7 @@ class ELOPlayer:
         if model is not None:
             model.eval()
             model.to(self.device)
-            self.evaluator = evaluator if evaluator is not None else LeafEvaluator(
+            self.evaluator = evaluator if evaluator is not None else leaf_evaluator(
                 model, dtype=nn_dtype, device=self.device)
 
     def reset(self):

@@ -138,6 +138,59 @@ def pack_resnet_params(net: AlphaZeroNetwork) -> torch.Tensor:
     return torch.cat(parts).contiguous()
 
 
+def h2_covers(net: nn.Module, dtype=torch.float32, device=None) -> bool:
+    """True when the h2 kernels evaluate `net`: fp32, an 8x8 or 6x6 AlphaZeroNetwork of 64 or 128
+    filters (the reference's configs: C2/C5 6x64, C3/C4 10x128, ModelConfig's 5x128), on a HIP
+    device."""
+    dev = torch.device(device) if device is not None else next(net.parameters()).device
+    return (dev.type == "cuda" and dtype == torch.float32 and
+            getattr(net, "board_size", None) in (6, 8) and
+            getattr(net, "num_filters", None) in (64, 128) and hasattr(net, "res_blocks"))
+
+
+class ModuleEvaluator:
+    """The leaf evaluator of a net the h2 kernels do not cover (another filter count, or any
+    module with the reference's forward): the module itself on the GPU through PyTorch-ROCm —
+    the north star's "leaf evaluation calls the existing ResNet via PyTorch-ROCm" — in fp32,
+    eval mode, logits and value as the expand wants them. Pull-style only (Engine.play runs the
+    h2 kernels inside its launch). Its rows may depend on the batch they share (the GEMM /
+    convolution algorithm MIOpen picks per shape), so callers do not memo its outputs
+    (SelfPlay and ELOPlayer turn the memo on for LeafEvaluator only)."""
+    kernel = "module"
+    accepts_live_count = False
+
+    def __init__(self, net: nn.Module, device=None):
+        dev = torch.device(device) if device is not None else next(net.parameters()).device
+        if dev.type != "cuda":
+            from . import _lib
+            raise _lib.RvzError("ModuleEvaluator runs the net on a HIP device (no CPU fallback)")
+        self.net, self.device = net.eval().to(dev), dev
+        self.board_size = int(getattr(net, "board_size", 8))
+
+    def __call__(self, x: torch.Tensor):
+        with torch.no_grad():
+            logits, value = self.net(x.float())
+        return logits.float().contiguous(), value.float().reshape(-1).contiguous()
+
+    def overflowed(self) -> bool:
+        return False
+
+
+def leaf_evaluator(net: nn.Module, dtype=torch.float32, device=None):
+    """The default leaf evaluator of SelfPlay / ELOPlayer: LeafEvaluator (the h2 kernels) when
+    they cover the net (h2_covers), else ModuleEvaluator, with a warning naming the shape."""
+    if h2_covers(net, dtype, device):
+        return LeafEvaluator(net, dtype=dtype, device=device)
+    import warnings
+    warnings.warn(f"rvz: the h2 kernels cover 64 / 128 filters in fp32; this net "
+                  f"({getattr(net, 'num_filters', '?')} filters, {dtype}) is evaluated by its "
+                  "PyTorch module on the GPU (ModuleEvaluator, pull-style)", stacklevel=2)
+    if dtype != torch.float32:
+        from . import _lib
+        raise _lib.RvzError("leaf evaluation is fp32 (the reference's precision)")
+    return ModuleEvaluator(net, device=device)
+
+
 class LeafEvaluator:
     """The leaf evaluator of the self-play path: the reference's forward (network.py:30-117,
     eval-mode BN folded) as the rvz h2 kernels — one trunk launch (k_resnet_h2: fp32 as a two-part
@@ -160,15 +213,14 @@ class LeafEvaluator:
         if kernel not in ("auto", "h2"):
             raise ValueError(f"unknown kernel {kernel!r}: the product evaluator is 'h2' "
                              "(A/B alternatives: tools/alt/alt_eval.py AltEvaluator)")
-        if not (dev.type == "cuda" and dtype == torch.float32 and net.board_size in (6, 8)
-                and net.num_filters in (64, 128)):
+        if not h2_covers(net, dtype, dev):
             raise _lib.RvzError(
                 "LeafEvaluator needs fp32, an 8x8 or 6x6 net of 64 or 128 filters and a HIP "
                 f"device (got {net.board_size}x{net.board_size}, {net.num_filters} filters, "
                 f"{dtype}, {dev}; no CPU fallback). For another shape hand the caller any "
-                "callable leaf_x -> (logits, value): rvz.SelfPlay(model, args, evaluator=...), "
-                "ELOPlayer(..., evaluator=...), e.g. evaluator=lambda x: model(x) "
-                "(INTEGRATION.md)")
+                "callable leaf_x -> (logits, value), e.g. rvz.ModuleEvaluator(model) "
+                "(SelfPlay / ELOPlayer pick it by themselves: rvz.network.leaf_evaluator; "
+                "INTEGRATION.md)")
         self.kernel = "h2"
         # bench.py: (int64 [ring, grid, 2] stamp ring, int32 [1] device launch counter) to time
         # every h2 trunk launch from device wall-clock stamps, or None

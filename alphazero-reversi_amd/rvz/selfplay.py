@@ -324,7 +324,8 @@ class SelfPlay:
     """
 
     def __init__(self, model, args: dict, evaluator: Optional[Callable] = None):
-        """evaluator: the leaf evaluator (default: LeafEvaluator(model), the fp32 h2 kernel).
+        """evaluator: the leaf evaluator (default: rvz.network.leaf_evaluator(model): the fp32 h2
+        kernels, or for a net they do not cover the module on the GPU, ModuleEvaluator).
         Any callable leaf_x -> (logits, value) works; with ``outputs_probs = True`` it returns
         softmaxed rows instead of logits, and a ``bind(engine)`` method is called with each new
         engine (tests replay the reference's recorded NN outputs this way).
@@ -332,7 +333,7 @@ class SelfPlay:
         of a pass is played to its end in ONE rvz_play launch (Engine.play: search, the h2 trunk
         and heads, act, records) instead of the pull-style ply loop; the same games, bit for bit
         (tests/test_gpu_dropin.py). Another evaluator always runs pull-style."""
-        from .network import LeafEvaluator
+        from .network import LeafEvaluator, leaf_evaluator
         self.model = model
         self.device = next(model.parameters()).device
         if self.device.type != "cuda":
@@ -340,7 +341,7 @@ class SelfPlay:
             self.model = model.to(self.device)
         self.model.eval()
         self.args = args
-        self.evaluator = evaluator if evaluator is not None else LeafEvaluator(
+        self.evaluator = evaluator if evaluator is not None else leaf_evaluator(
             self.model, dtype=args.get("nn_dtype", torch.float32), device=self.device)
         self.board_size = int(getattr(model, "board_size", 8))
         self.save_dir = args.get("save_dir", "self_play_data")

@@ -107,3 +107,22 @@ def test_seeded_6x64_net_reproduces_reference_fixture():
     with torch.no_grad():
         v64 = net64(torch.from_numpy(x).double())[1].numpy().reshape(-1)
     assert np.abs(value - v64).max() <= 5e-5 and np.abs(v - v64).max() <= 5e-5
+
+
+def test_default_leaf_evaluator_choice():
+    """rvz.network.leaf_evaluator (SelfPlay's / ELOPlayer's default): the h2 kernels for fp32
+    8x8 / 6x6 nets of 64 or 128 filters on a HIP device, the module on the GPU
+    (ModuleEvaluator) for any other width, never a CPU path."""
+    import pytest
+    import torch
+    import rvz
+    from rvz.network import h2_covers, leaf_evaluator
+    for f, want in ((64, True), (128, True), (32, False), (256, False)):
+        net = rvz.AlphaZeroNetwork(8, 1, f)
+        assert h2_covers(net, torch.float32, "cuda") is want, f
+        assert not h2_covers(net, torch.float32, "cpu")
+        assert not h2_covers(net, torch.bfloat16, "cuda")
+    assert h2_covers(rvz.AlphaZeroNetwork(6, 1, 64), torch.float32, "cuda")
+    with pytest.warns(UserWarning, match="ModuleEvaluator"):
+        with pytest.raises(rvz.RvzError, match="HIP device"):
+            leaf_evaluator(rvz.AlphaZeroNetwork(8, 1, 32), device="cpu")
