@@ -261,13 +261,14 @@ def test_selfplay_with_a_net_the_h2_kernels_do_not_cover(tmp_path, oracle):
     PyTorch-ROCm), pull-style, with a warning. The games are the reference's for that evaluator:
     the oracle's one-game-after-another restatement fed the same module's outputs (row by row,
     softmaxed by the expand's own softmax) plays the same moves, policies and values, as long as
-    the module's rows do not depend on the batch they share (checked first, per row)."""
+    the module's rows do not depend on the batch they share (checked first, per row). 800
+    simulations: the net decides the moves whenever the root has fewer than 12 legal moves."""
     import rvz
     from oracle_play import reference_generate_games
     torch.manual_seed(0)
     net = rvz.AlphaZeroNetwork(8, 2, 32).cuda().eval()
     with pytest.warns(UserWarning, match="ModuleEvaluator"):
-        sp = rvz.SelfPlay(net, {"num_simulations": 200, "save_dir": str(tmp_path)})
+        sp = rvz.SelfPlay(net, {"num_simulations": 800, "save_dir": str(tmp_path)})
     assert isinstance(sp.evaluator, rvz.ModuleEvaluator) and not sp.fused
     np.random.seed(3)
     got = sp.generate_games(6)
@@ -289,7 +290,7 @@ def test_selfplay_with_a_net_the_h2_kernels_do_not_cover(tmp_path, oracle):
         logits, value = sp.evaluator(torch.from_numpy(xs).cuda())
         return rvz.policy_softmax(logits, 8).cpu().numpy(), value.cpu().numpy()
 
-    want = reference_generate_games(oracle, 6, 200, 1.0, np.random.RandomState(3), evaluate)
+    want = reference_generate_games(oracle, 6, 800, 1.0, np.random.RandomState(3), evaluate)
     for a, b in zip(got, want):
         assert a["current_players"] == b["current_players"] and a["winner"] == b["winner"]
         for p, q in zip(a["action_probs"], b["action_probs"]):
