@@ -153,24 +153,35 @@ class ModuleEvaluator:
     module with the reference's forward): the module itself on the GPU through PyTorch-ROCm —
     the north star's "leaf evaluation calls the existing ResNet via PyTorch-ROCm" — in fp32,
     eval mode, logits and value as the expand wants them. Pull-style only (Engine.play runs the
-    h2 kernels inside its launch). Its rows may depend on the batch they share (the GEMM /
-    convolution algorithm MIOpen picks per shape), so callers do not memo its outputs
-    (SelfPlay and ELOPlayer turn the memo on for LeafEvaluator only)."""
+    h2 kernels inside its launch). MIOpen picks its convolution algorithm per tensor shape, so a
+    row's outputs would depend on how many rows share the call; the module therefore always runs
+    on chunks of exactly `chunk` rows (the last one zero-padded): one shape, one algorithm, and
+    every row's outputs a function of that row alone, as the engine's memo and the oracle
+    comparisons assume (tests/test_gpu_dropin.py)."""
     kernel = "module"
     accepts_live_count = False
 
-    def __init__(self, net: nn.Module, device=None):
+    def __init__(self, net: nn.Module, device=None, chunk: int = 64):
         dev = torch.device(device) if device is not None else next(net.parameters()).device
         if dev.type != "cuda":
             from . import _lib
             raise _lib.RvzError("ModuleEvaluator runs the net on a HIP device (no CPU fallback)")
-        self.net, self.device = net.eval().to(dev), dev
+        self.net, self.device, self.chunk = net.eval().to(dev), dev, int(chunk)
         self.board_size = int(getattr(net, "board_size", 8))
 
     def __call__(self, x: torch.Tensor):
+        n, c = x.shape[0], self.chunk
+        xp = x.float()
+        if n % c:
+            xp = torch.cat([xp, xp.new_zeros((c - n % c,) + tuple(x.shape[1:]))])
+        outs = []
         with torch.no_grad():
-            logits, value = self.net(x.float())
-        return logits.float().contiguous(), value.float().reshape(-1).contiguous()
+            for i in range(0, xp.shape[0], c):
+                lg, v = self.net(xp[i:i + c])
+                outs.append((lg.float(), v.float().reshape(-1)))
+        logits = torch.cat([o[0] for o in outs])[:n].contiguous()
+        value = torch.cat([o[1] for o in outs])[:n].contiguous()
+        return logits, value
 
     def overflowed(self) -> bool:
         return False
