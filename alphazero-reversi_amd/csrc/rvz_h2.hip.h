@@ -637,39 +637,78 @@ __device__ __forceinline__ void conv_h2(const uint16_t* __restrict__ in, uint16_
                 aq[u][p] = *reinterpret_cast<const f16x8*>(ap + p * C::PLANE);
         }
     };
-    f16x8 bq[NIT + PD][CTW][2];
-    f16x8 aq[APD + 1][PTW][2];
+    if constexpr (NIT <= 48) {   // F = 64, 128: the whole k-loop unrolled, one slot per k-step
+        f16x8 bq[NIT + PD][CTW][2];
+        f16x8 aq[APD + 1][PTW][2];
 #pragma unroll
-    for (int d = 0; d < PD; ++d)
+        for (int d = 0; d < PD; ++d)
 #pragma unroll
-        for (int c = 0; c < CTW; ++c)
+            for (int c = 0; c < CTW; ++c)
 #pragma unroll
-            for (int p = 0; p < 2; ++p) bq[d][c][p] = bc[d][c][p];
+                for (int p = 0; p < 2; ++p) bq[d][c][p] = bc[d][c][p];
 #pragma unroll
-    for (int d = 0; d < APD; ++d) load_a(aq[d], d);
+        for (int d = 0; d < APD; ++d) load_a(aq[d], d);
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-        const int ia = it + APD;                      // the A operands loaded this k-step
-        if (ia < NIT) load_a(aq[ia % (APD + 1)], ia);
-        load_b(bq[it + PD], it + PD);
-        const bool sa = ia < NIT && skip0(ia);        // next A load without tile 0
-        if (skip0(it)) {
-            mma3<CTW, PTW, 1>(acc, aq[it % (APD + 1)], bq[it]);
-            if (sa) interleave_loads<0, 3 * CTW * (PTW - 1), 2 * (PTW - 1), 2 * CTW>();
-            else interleave_loads<0, 3 * CTW * (PTW - 1), 2 * PTW, 2 * CTW>();
-        } else {
-            mma3(acc, aq[it % (APD + 1)], bq[it]);
-            if (sa) interleave_loads<0, 3 * CTW * PTW, 2 * (PTW - 1), 2 * CTW>();
-            else interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+        for (int it = 0; it < NIT; ++it) {
+            const int ia = it + APD;                  // the A operands loaded this k-step
+            if (ia < NIT) load_a(aq[ia % (APD + 1)], ia);
+            load_b(bq[it + PD], it + PD);
+            const bool sa = ia < NIT && skip0(ia);    // next A load without tile 0
+            if (skip0(it)) {
+                mma3<CTW, PTW, 1>(acc, aq[it % (APD + 1)], bq[it]);
+                if (sa) interleave_loads<0, 3 * CTW * (PTW - 1), 2 * (PTW - 1), 2 * CTW>();
+                else interleave_loads<0, 3 * CTW * (PTW - 1), 2 * PTW, 2 * CTW>();
+            } else {
+                mma3(acc, aq[it % (APD + 1)], bq[it]);
+                if (sa) interleave_loads<0, 3 * CTW * PTW, 2 * (PTW - 1), 2 * CTW>();
+                else interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+            }
+            __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int d = 0; d < PD; ++d)
+#pragma unroll
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
+    } else {
+        // F = 256 (72 k-steps of 48 MFMAs): a fully unrolled loop exceeds the unroller's budget
+        // and a per-k-step register array indexed at run time lives in scratch. Weight fragments
+        // rotate through PD + 1 slots and activations through APD + 1; the loop runs in chunks of
+        // U k-steps (a multiple of both ring lengths), so every slot index inside a chunk is a
+        // compile-time constant. No ILV here (one board per workgroup): no tile-0 skips.
+        static_assert(!ILV, "the chunked k-loop has no tile-0 skip window");
+        constexpr int RB = PD + 1, RA = APD + 1, U = 24;
+        static_assert(NIT % U == 0 && U % RB == 0 && U % RA == 0, "k-loop chunking");
+        f16x8 bq[RB][CTW][2];
+        f16x8 aq[RA][PTW][2];
+#pragma unroll
+        for (int d = 0; d < PD; ++d)
+#pragma unroll
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) bq[d][c][p] = bc[d][c][p];
+#pragma unroll
+        for (int d = 0; d < APD; ++d) load_a(aq[d], d);
+#pragma unroll 1
+        for (int o = 0; o < NIT; o += U) {
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const int it = o + j, ia = it + APD;
+                if (ia < NIT) load_a(aq[(j + APD) % RA], ia);
+                load_b(bq[(j + PD) % RB], it + PD);
+                mma3(acc, aq[j % RA], bq[j % RB]);
+                interleave_loads<0, 3 * CTW * PTW, 2 * PTW, 2 * CTW>();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < PD; ++d)
+#pragma unroll
+            for (int c = 0; c < CTW; ++c)
+#pragma unroll
+                for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[(NIT + d) % RB][c][p];
     }
-#pragma unroll
-    for (int d = 0; d < PD; ++d)
-#pragma unroll
-        for (int c = 0; c < CTW; ++c)
-#pragma unroll
-            for (int p = 0; p < 2; ++p) bc[d][c][p] = bq[NIT + d][c][p];
     // conv A (block input -> t): the skip input stays in er.res; conv B adds it and keeps
     epilogue_h2<F, G::NPIX, CTW, PTW, RES, RES, G>(out, acc, er, wt, lane, wave, ovf, rg, sin, sout,
                                                    rm_out, ovw);
@@ -773,7 +812,7 @@ __device__ __forceinline__ RangeS<NBOARD> h2_trunk(char* smem, const float* __re
     float* xin = reinterpret_cast<float*>(actB);     // free until the first conv writes B
     const H2W wr(blob, h2_blob_elems(F, n_blocks));
     const RangeLds rl{reinterpret_cast<float*>(smem + C::RMAX)};
-    constexpr int PD = RG ? 1 : RVZ_H2_PD, APD = RG ? 0 : RVZ_H2_APD;
+    constexpr int PD = RG || F == 256 ? 1 : RVZ_H2_PD, APD = RG ? 0 : RVZ_H2_APD;
     PASS_NOW(tp0);
     f16x8 bc[PD][CTW][2];
     if (n_blocks > 0) {

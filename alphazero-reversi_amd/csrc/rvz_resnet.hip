@@ -218,17 +218,25 @@ static void launch_trunk_h2(const float* x, int32_t n, const float* params, cons
         hipLaunchKernelGGL((k_resnet_h2<64, 2, 2, 4, 8, 2>), grid, dim3(256), 0, s, x, n,
                            params, L, blob, blocks, work, n_live, stamps, stamp_ctr, ring,
                            claim);
-    else
+    else if (filters == 128)
         hipLaunchKernelGGL((k_resnet_h2<128, 1, 2, 4, 8, 2>), grid, dim3(256), 0, s, x, n, params,
+                           L, blob, blocks, work, n_live, stamps, stamp_ctr, ring, claim);
+    else   // F=256: the F=128 tile map with 4 channel tiles per wave; 144 KB of LDS, 1 per CU
+        hipLaunchKernelGGL((k_resnet_h2<256, 1, 4, 4, 8, 1>), grid, dim3(256), 0, s, x, n, params,
                            L, blob, blocks, work, n_live, stamps, stamp_ctr, ring, claim);
 }
 
 extern "C" {
 
 static bool board_ok(int32_t bs) { return bs == 8 || bs == 6; }
+// trunk widths with an h2 instantiation: 64 and 128 on both boards, 256 on 8x8
+static bool width_ok(int32_t filters) { return filters == 64 || filters == 128 || filters == 256; }
+static bool trunk_ok(int32_t bs, int32_t filters) {
+    return board_ok(bs) && (filters == 64 || filters == 128 || (filters == 256 && bs == 8));
+}
 
 int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks) {
-    if ((filters != 64 && filters != 128) || blocks < 0 || !board_ok(board)) return RVZ_EINVAL;
+    if (!width_ok(filters) || blocks < 0 || !board_ok(board)) return RVZ_EINVAL;
     return make_layout(filters, blocks, board).total;
 }
 #ifdef RVZ_PHASE_TIMING
@@ -261,7 +269,7 @@ int rvz_resnet_heads_fc_ex(int32_t board, const float* work, int32_t n, const fl
                            const int32_t* n_live, uint32_t* stamp_ctr, void* stream) {
     const rvz::Range trace_range("rvz.eval.heads (k_heads_mfma)");
     if (!work || !params || !logits || !value || n < 0 || blocks < 0 || !board_ok(board) ||
-        (filters != 64 && filters != 128))
+        !width_ok(filters))
         return RVZ_EINVAL;
     // the heads copy workspace rows as f32x4: a misaligned workspace is an argument error, not
     // a device fault
@@ -285,13 +293,13 @@ int rvz_resnet_heads_fc(int32_t board, const float* work, int32_t n, const float
                                   nullptr, stream);
 }
 int64_t rvz_resnet_h2_size(int32_t filters, int32_t blocks) {
-    if ((filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
+    if (!width_ok(filters) || blocks < 0) return RVZ_EINVAL;
     return h2_blob_elems(filters, blocks);
 }
 
 int rvz_resnet_h2_weights(const float* params, int32_t filters, int32_t blocks, uint16_t* blob,
                           void* stream) {
-    if (!params || !blob || (filters != 64 && filters != 128) || blocks < 0) return RVZ_EINVAL;
+    if (!params || !blob || !width_ok(filters) || blocks < 0) return RVZ_EINVAL;
     if (((uintptr_t)blob & 15) != 0) return RVZ_EINVAL;
     hipStream_t s = (hipStream_t)stream;
     const Layout L = make_layout(filters, blocks);
@@ -314,8 +322,8 @@ int rvz_resnet_trunk_h2_ex(int32_t board, const float* x, int32_t n, const float
                            const int32_t* n_live, uint64_t* stamps, const uint32_t* stamp_ctr,
                            int32_t ring, void* stream) {
     const rvz::Range trace_range("rvz.eval.trunk (k_resnet_h2)");
-    if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !board_ok(board) ||
-        (filters != 64 && filters != 128) || (stamp_ctr && (!stamps || ring <= 0)))
+    if (!x || !params || !blob || !work || n < 0 || blocks < 0 || !trunk_ok(board, filters) ||
+        (stamp_ctr && (!stamps || ring <= 0)))
         return RVZ_EINVAL;
     // work: 16-byte aligned (the 64-bit unit-counter atomic at words n*192 + 2, 3 and the
     // heads' f32x4 row copies)
@@ -341,7 +349,7 @@ int rvz_resnet_trunk_h2(int32_t board, const float* x, int32_t n, const float* p
 }
 
 int32_t rvz_resnet_h2_grid(int32_t board, int32_t filters, int32_t n) {
-    if (!board_ok(board) || (filters != 64 && filters != 128) || n < 0) return RVZ_EINVAL;
+    if (!trunk_ok(board, filters) || n < 0) return RVZ_EINVAL;
     return h2_grid(board, filters, n);
 }
 

@@ -138,14 +138,19 @@ def pack_resnet_params(net: AlphaZeroNetwork) -> torch.Tensor:
     return torch.cat(parts).contiguous()
 
 
+H2_WIDTHS = {8: (64, 128, 256), 6: (64, 128)}   # trunk widths with an h2 instantiation
+PLAY_WIDTHS = (64, 128)                          # ... and with a fused k_play (Engine.play)
+
+
 def h2_covers(net: nn.Module, dtype=torch.float32, device=None) -> bool:
-    """True when the h2 kernels evaluate `net`: fp32, an 8x8 or 6x6 AlphaZeroNetwork of 64 or 128
-    filters (the reference's configs: C2/C5 6x64, C3/C4 10x128, ModelConfig's 5x128), on a HIP
-    device."""
+    """True when the h2 kernels evaluate `net`: fp32, an 8x8 AlphaZeroNetwork of 64, 128 or 256
+    filters or a 6x6 one of 64 or 128 (the reference's configs: C2/C5 6x64, C3/C4 10x128,
+    ModelConfig's 5x128; 256 = network.py's wider towers), on a HIP device."""
     dev = torch.device(device) if device is not None else next(net.parameters()).device
     return (dev.type == "cuda" and dtype == torch.float32 and
-            getattr(net, "board_size", None) in (6, 8) and
-            getattr(net, "num_filters", None) in (64, 128) and hasattr(net, "res_blocks"))
+            getattr(net, "num_filters", None) in H2_WIDTHS.get(getattr(net, "board_size", None),
+                                                               ()) and
+            hasattr(net, "res_blocks"))
 
 
 class ModuleEvaluator:
@@ -193,7 +198,7 @@ def leaf_evaluator(net: nn.Module, dtype=torch.float32, device=None):
     if h2_covers(net, dtype, device):
         return LeafEvaluator(net, dtype=dtype, device=device)
     import warnings
-    warnings.warn(f"rvz: the h2 kernels cover 64 / 128 filters in fp32; this net "
+    warnings.warn(f"rvz: the h2 kernels cover 64 / 128 (and on 8x8 256) filters in fp32; this net "
                   f"({getattr(net, 'num_filters', '?')} filters, {dtype}) is evaluated by its "
                   "PyTorch module on the GPU (ModuleEvaluator, pull-style)", stacklevel=2)
     if dtype != torch.float32:
@@ -208,7 +213,8 @@ class LeafEvaluator:
     f16 split, three partial products on the f16 MFMA) and one FC-heads launch (k_heads_mfma) per
     leaf batch. Returns (logits f32 [n, S*S+1], value f32 [n]); the rvz expand kernel reads them
     directly (it fuses the softmax). fp32 only (the reference's precision), 8x8 or 6x6 boards,
-    64 or 128 filters, on the GPU: anything else raises (no CPU or PyTorch fallback). The A/B
+    64 or 128 filters, or 256 on 8x8 (pull-style only: the fused k_play instantiates 64 and 128),
+    on the GPU: anything else raises (no CPU or PyTorch fallback). The A/B
     alternatives (exact f32 MFMA, 3-part bf16 split, MIOpen) live in tools/alt (AltEvaluator).
     """
 
@@ -226,7 +232,8 @@ class LeafEvaluator:
                              "(A/B alternatives: tools/alt/alt_eval.py AltEvaluator)")
         if not h2_covers(net, dtype, dev):
             raise _lib.RvzError(
-                "LeafEvaluator needs fp32, an 8x8 or 6x6 net of 64 or 128 filters and a HIP "
+                "LeafEvaluator needs fp32, an 8x8 or 6x6 net of 64 or 128 filters (or 8x8 of "
+                "256) and a HIP "
                 f"device (got {net.board_size}x{net.board_size}, {net.num_filters} filters, "
                 f"{dtype}, {dev}; no CPU fallback). For another shape hand the caller any "
                 "callable leaf_x -> (logits, value), e.g. rvz.ModuleEvaluator(model) "

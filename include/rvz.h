@@ -299,7 +299,8 @@ int rvz_footprint(const rvz_engine *e, int64_t *bytes_tree, int64_t *bytes_env);
  * [n, 3, board, board] (the leaf planes) -> logits float32 [n, board^2 + 1], value float32 [n].
  * params: the packed fp32 buffer laid out as in csrc/rvz_resnet_common.hip.h
  * (rvz.network.pack_resnet_params), 16-byte aligned, of rvz_resnet_params_size(board, filters,
- * blocks) floats (negative: unsupported shape). filters 64 or 128, any block count.
+ * blocks) floats (negative: unsupported shape). filters 64 or 128 (boards 8 and 6) or 256 (board
+ * 8: the h2 trunk; the fused rvz_play takes 64 and 128), any block count.
  * work: float scratch of rvz_resnet_work_size(n) elements (the 1x1-conv head outputs handed from
  * the trunk launch to the FC-heads launch, + the overflow word). */
 int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks);

@@ -295,3 +295,33 @@ def test_selfplay_with_a_net_the_h2_kernels_do_not_cover(tmp_path, oracle):
         assert a["current_players"] == b["current_players"] and a["winner"] == b["winner"]
         for p, q in zip(a["action_probs"], b["action_probs"]):
             assert np.array_equal(p, q)
+
+
+def test_selfplay_with_a_256_filter_net(tmp_path, oracle):
+    """A 256-filter 8x8 net (network.py's widths are a constructor argument): the default
+    evaluator is the h2 LeafEvaluator (k_resnet_h2<256, ...>), pull-style (the fused k_play
+    instantiates 64 and 128), and the games are the oracle's one-game-after-another restatement
+    fed that evaluator's outputs: same moves, policies and values, at 800 simulations."""
+    import rvz
+    from oracle_play import reference_generate_games
+    torch.manual_seed(1)
+    net = rvz.AlphaZeroNetwork(8, 1, 256).cuda().eval()
+    sp = rvz.SelfPlay(net, {"num_simulations": 800, "save_dir": str(tmp_path)})
+    assert isinstance(sp.evaluator, rvz.LeafEvaluator) and sp.evaluator.filters == 256
+    assert not sp.fused
+    with pytest.raises(ValueError):
+        rvz.SelfPlay(net, {"num_simulations": 8, "save_dir": str(tmp_path), "fused": True})
+    np.random.seed(4)
+    got = sp.generate_games(4)
+    assert len({g["states"][4].tobytes() for g in got}) > 1
+
+    def evaluate(xs):
+        logits, value = sp.evaluator(torch.from_numpy(xs).cuda())
+        return rvz.policy_softmax(logits, 8).cpu().numpy(), value.cpu().numpy()
+
+    want = reference_generate_games(oracle, 4, 800, 1.0, np.random.RandomState(4), evaluate)
+    for a, b in zip(got, want):
+        assert a["current_players"] == b["current_players"] and a["winner"] == b["winner"]
+        for p, q in zip(a["action_probs"], b["action_probs"]):
+            assert np.array_equal(p, q)
+    assert not sp.evaluator.overflowed()

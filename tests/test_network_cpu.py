@@ -111,18 +111,19 @@ def test_seeded_6x64_net_reproduces_reference_fixture():
 
 def test_default_leaf_evaluator_choice():
     """rvz.network.leaf_evaluator (SelfPlay's / ELOPlayer's default): the h2 kernels for fp32
-    8x8 / 6x6 nets of 64 or 128 filters on a HIP device, the module on the GPU
-    (ModuleEvaluator) for any other width, never a CPU path."""
+    8x8 / 6x6 nets of 64 or 128 filters and 8x8 nets of 256 on a HIP device, the module on the
+    GPU (ModuleEvaluator) for any other shape, never a CPU path."""
     import pytest
     import torch
     import rvz
     from rvz.network import h2_covers, leaf_evaluator
-    for f, want in ((64, True), (128, True), (32, False), (256, False)):
+    for f, want in ((64, True), (128, True), (32, False), (256, True), (512, False)):
         net = rvz.AlphaZeroNetwork(8, 1, f)
         assert h2_covers(net, torch.float32, "cuda") is want, f
         assert not h2_covers(net, torch.float32, "cpu")
         assert not h2_covers(net, torch.bfloat16, "cuda")
     assert h2_covers(rvz.AlphaZeroNetwork(6, 1, 64), torch.float32, "cuda")
+    assert not h2_covers(rvz.AlphaZeroNetwork(6, 1, 256), torch.float32, "cuda")
     with pytest.warns(UserWarning, match="ModuleEvaluator"):
         with pytest.raises(rvz.RvzError, match="HIP device"):
             leaf_evaluator(rvz.AlphaZeroNetwork(8, 1, 32), device="cpu")
