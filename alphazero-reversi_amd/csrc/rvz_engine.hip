@@ -1860,7 +1860,8 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     if (!e || !a) return RVZ_EINVAL;
     if (!a->params || !a->blob || !a->scratch || !a->seeds || !a->plies_done || !a->out_idx ||
         !a->out_p || (a->reset && !a->games_done) || a->plies < 1 || a->blocks < 0 ||
-        (a->filters != 64 && a->filters != 128) || a->games_per_workgroup < -PLAY_GPW_MAX ||
+        (a->filters != 64 && a->filters != 128 && !(a->filters == 256 && e->BS == 8)) ||
+        a->games_per_workgroup < -PLAY_GPW_MAX ||
         e->cfg.leaf_dtype != RVZ_LEAF_F32) {
         e->err = "rvz_play: invalid arguments";
         return RVZ_EINVAL;
@@ -1986,8 +1987,9 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     if (const char* sl = getenv("RVZ_PLAY_SPIN_LIMIT")) pa.spin_limit = (unsigned)strtoul(sl, nullptr, 10);
     e->searching = 0;
     if (e->BS == 8)
-        return a->filters == 64 ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)
-                                : play_launch<128, 1, 2, 4, 8, 2>(e, v, pa, 2);
+        return a->filters == 64    ? play_launch<64, 2, 2, 4, 8, 2>(e, v, pa, 2)
+               : a->filters == 128 ? play_launch<128, 1, 2, 4, 8, 2>(e, v, pa, 2)
+                                   : play_launch<256, 1, 4, 4, 8, 1>(e, v, pa, 1);
     return a->filters == 64 ? play_launch<64, 3, 2, 4, 6, 2>(e, v, pa, 2)
                             : play_launch<128, 1, 2, 3, 6, 2>(e, v, pa, 2);
 }

@@ -138,8 +138,8 @@ def pack_resnet_params(net: AlphaZeroNetwork) -> torch.Tensor:
     return torch.cat(parts).contiguous()
 
 
-H2_WIDTHS = {8: (64, 128, 256), 6: (64, 128)}   # trunk widths with an h2 instantiation
-PLAY_WIDTHS = (64, 128)                          # ... and with a fused k_play (Engine.play)
+# trunk widths with an h2 instantiation (k_resnet_h2 and the fused k_play alike)
+H2_WIDTHS = {8: (64, 128, 256), 6: (64, 128)}
 
 
 def h2_covers(net: nn.Module, dtype=torch.float32, device=None) -> bool:
@@ -213,8 +213,7 @@ class LeafEvaluator:
     f16 split, three partial products on the f16 MFMA) and one FC-heads launch (k_heads_mfma) per
     leaf batch. Returns (logits f32 [n, S*S+1], value f32 [n]); the rvz expand kernel reads them
     directly (it fuses the softmax). fp32 only (the reference's precision), 8x8 or 6x6 boards,
-    64 or 128 filters, or 256 on 8x8 (pull-style only: the fused k_play instantiates 64 and 128),
-    on the GPU: anything else raises (no CPU or PyTorch fallback). The A/B
+    64 or 128 filters, or 256 on 8x8, on the GPU: anything else raises (no CPU or PyTorch fallback). The A/B
     alternatives (exact f32 MFMA, 3-part bf16 split, MIOpen) live in tools/alt (AltEvaluator).
     """
 

@@ -329,12 +329,11 @@ class SelfPlay:
         Any callable leaf_x -> (logits, value) works; with ``outputs_probs = True`` it returns
         softmaxed rows instead of logits, and a ``bind(engine)`` method is called with each new
         engine (tests replay the reference's recorded NN outputs this way).
-        args["fused"] (default: True with the h2 LeafEvaluator of a 64- or 128-filter net, the
-        default evaluator): every game of a pass is played to its end in ONE rvz_play launch
-        (Engine.play: search, the h2 trunk and heads, act, records) instead of the pull-style ply
-        loop; the same games, bit for bit (tests/test_gpu_dropin.py). Another evaluator, or the
-        h2 evaluator of a 256-filter net, runs pull-style."""
-        from .network import PLAY_WIDTHS, LeafEvaluator, leaf_evaluator
+        args["fused"] (default: True with the h2 LeafEvaluator, the default evaluator): every game
+        of a pass is played to its end in ONE rvz_play launch (Engine.play: search, the h2 trunk
+        and heads, act, records) instead of the pull-style ply loop; the same games, bit for bit
+        (tests/test_gpu_dropin.py). Another evaluator always runs pull-style."""
+        from .network import LeafEvaluator, leaf_evaluator
         self.model = model
         self.device = next(model.parameters()).device
         if self.device.type != "cuda":
@@ -348,13 +347,10 @@ class SelfPlay:
         self.save_dir = args.get("save_dir", "self_play_data")
         os.makedirs(self.save_dir, exist_ok=True)
         self.seed = None if args.get("seed") is None else int(args["seed"])
-        playable = (isinstance(self.evaluator, LeafEvaluator) and
-                     self.evaluator.filters in PLAY_WIDTHS)
-        self.fused = bool(args.get("fused", playable))
-        if self.fused and not playable:
-            raise ValueError("SelfPlay: args['fused'] plays the h2 LeafEvaluator of a 64- or "
-                             "128-filter net inside the launch; another evaluator goes through "
-                             "the pull-style loop")
+        self.fused = bool(args.get("fused", isinstance(self.evaluator, LeafEvaluator)))
+        if self.fused and not isinstance(self.evaluator, LeafEvaluator):
+            raise ValueError("SelfPlay: args['fused'] plays the h2 LeafEvaluator inside the "
+                             "launch; another evaluator goes through the pull-style loop")
         self.games_played = 0
         self.reference_order_passes = 0
 

@@ -331,6 +331,7 @@ DISPATCHES = []      # (kernel instantiation, label, ms)
 def play_kernel(board, filters):
     """rvz_play's kernel instantiation for a geometry (csrc/rvz_engine.hip rvz_play)."""
     return {(8, 64): "k_play<64, 2, 2, 4, 8, 2>", (8, 128): "k_play<128, 1, 2, 4, 8, 2>",
+            (8, 256): "k_play<256, 1, 4, 4, 8, 1>",
             (6, 64): "k_play<64, 3, 2, 4, 6, 2>", (6, 128): "k_play<128, 1, 2, 3, 6, 2>"}[
         (board, filters)]
 
@@ -627,6 +628,14 @@ def cpu_baseline(args, net):
             "env_tree_only_1core": one}
 
 
+def preset_shape(args):
+    """True when the run's board, net and simulations are its preset's (the stored PMC passes and
+    clock were measured on the presets; an override such as --filters 256 makes them another
+    workload's)."""
+    p = PRESETS[args.config]
+    return all(getattr(args, k) == p[k] for k in ("board", "blocks", "filters", "sims") if k in p)
+
+
 def stored_traffic(args, kernel, plies=None):
     """HBM bytes per launch of `kernel` from the committed PMC passes (--pmc), quoted only for the
     configuration they were measured on, with their source named. k_play: key "play" (C2's
@@ -642,7 +651,7 @@ def stored_traffic(args, kernel, plies=None):
     key = f"play_{args.config}" if kernel == "play" and args.config != "c2" else kernel
     ent = pmc.get(key, {})
     games = ent.get("games", 4096)
-    if ent.get("config", "c2") != args.config or games != args.games:
+    if ent.get("config", "c2") != args.config or games != args.games or not preset_shape(args):
         return None, None
     b = ent.get("hbm_bytes_per_launch")
     if b is None:
@@ -667,7 +676,8 @@ def stored_pmc_clock(args):
         return None
     key = f"play_{args.config}" if args.config != "c2" else "play"
     ent = pmc.get(key, {})
-    if ent.get("config", "c2") != args.config or ent.get("games", 4096) != args.games:
+    if (ent.get("config", "c2") != args.config or ent.get("games", 4096) != args.games or
+            not preset_shape(args)):
         return None
     if "clock_GHz" not in ent:
         return None

@@ -196,7 +196,7 @@ int rvz_act(rvz_engine *e, double temperature, const double *u, int32_t apply, i
 typedef struct rvz_play_args {
     const float *params;         /* packed fp32 net (rvz_resnet_params_size layout) */
     const uint16_t *blob;        /* its h2 weight blob (rvz_resnet_h2_weights), 16-byte aligned */
-    int32_t filters;             /* 64 | 128 */
+    int32_t filters;             /* 64 | 128 (| 256 on board 8) */
     int32_t blocks;              /* residual blocks */
     float *scratch;              /* rvz_play_scratch_size(e) floats, 16-byte aligned */
     float *ovf;                  /* the evaluator's sticky f16-overflow word (set to 1), nullable */
@@ -300,7 +300,7 @@ int rvz_footprint(const rvz_engine *e, int64_t *bytes_tree, int64_t *bytes_env);
  * params: the packed fp32 buffer laid out as in csrc/rvz_resnet_common.hip.h
  * (rvz.network.pack_resnet_params), 16-byte aligned, of rvz_resnet_params_size(board, filters,
  * blocks) floats (negative: unsupported shape). filters 64 or 128 (boards 8 and 6) or 256 (board
- * 8: the h2 trunk; the fused rvz_play takes 64 and 128), any block count.
+ * 8; the fused rvz_play too), any block count.
  * work: float scratch of rvz_resnet_work_size(n) elements (the 1x1-conv head outputs handed from
  * the trunk launch to the FC-heads launch, + the overflow word). */
 int64_t rvz_resnet_params_size(int32_t board, int32_t filters, int32_t blocks);

@@ -195,3 +195,18 @@ def test_bench_world4_dry_run_ranks_cover_every_ply():
     for p in d["ranks"]["per_rank"]:
         assert p["stagger_plies"] == [0, 59], p
         assert p["stagger_games_per_ply"] == [8, 9], p
+
+
+def test_stored_pmc_quoted_only_for_the_preset_shape():
+    """bench.py quotes the committed PMC traffic and clock (profiles/pmc_traffic.json) only for
+    the workload they were measured on: the preset's games, board, net and simulations. An
+    override (--filters 256, --sims 400, --games ...) leaves roofline.traffic null."""
+    import bench
+    a = bench.parse(["--config", "c3"])
+    b, src = bench.stored_traffic(a, "play", plies=20)
+    assert b and "play_c3" in src
+    assert bench.stored_pmc_clock(a) is not None
+    for extra in (["--filters", "256"], ["--sims", "400"], ["--blocks", "5"], ["--games", "1024"]):
+        o = bench.parse(["--config", "c3"] + extra)
+        assert bench.stored_traffic(o, "play", plies=20) == (None, None), extra
+        assert bench.stored_pmc_clock(o) is None, extra

@@ -297,20 +297,23 @@ def test_selfplay_with_a_net_the_h2_kernels_do_not_cover(tmp_path, oracle):
             assert np.array_equal(p, q)
 
 
-def test_selfplay_with_a_256_filter_net(tmp_path, oracle):
+@pytest.mark.parametrize("fused", [True, False])
+def test_selfplay_with_a_256_filter_net(tmp_path, oracle, fused):
     """A 256-filter 8x8 net (network.py's widths are a constructor argument): the default
-    evaluator is the h2 LeafEvaluator (k_resnet_h2<256, ...>), pull-style (the fused k_play
-    instantiates 64 and 128), and the games are the oracle's one-game-after-another restatement
-    fed that evaluator's outputs: same moves, policies and values, at 800 simulations."""
+    evaluator is the h2 LeafEvaluator (k_resnet_h2<256, ...>), SelfPlay plays it fused by default
+    (k_play<256, ...>) or pull-style, and either way the games are the oracle's
+    one-game-after-another restatement fed that evaluator's outputs: same moves, policies and
+    values, at 800 simulations."""
     import rvz
     from oracle_play import reference_generate_games
     torch.manual_seed(1)
     net = rvz.AlphaZeroNetwork(8, 1, 256).cuda().eval()
-    sp = rvz.SelfPlay(net, {"num_simulations": 800, "save_dir": str(tmp_path)})
+    args = {"num_simulations": 800, "save_dir": str(tmp_path)}
+    if not fused:
+        args["fused"] = False
+    sp = rvz.SelfPlay(net, args)
     assert isinstance(sp.evaluator, rvz.LeafEvaluator) and sp.evaluator.filters == 256
-    assert not sp.fused
-    with pytest.raises(ValueError):
-        rvz.SelfPlay(net, {"num_simulations": 8, "save_dir": str(tmp_path), "fused": True})
+    assert sp.fused == fused
     np.random.seed(4)
     got = sp.generate_games(4)
     assert len({g["states"][4].tobytes() for g in got}) > 1

@@ -89,10 +89,12 @@ def test_fused_workgroup_sizes_and_launch_splits(gpw, chunks):
 
 
 @pytest.mark.parametrize("board,blocks,filters,gpw", [(8, 2, 128, 0), (8, 2, 128, -16),
-                                                     (6, 2, 64, 0), (6, 1, 128, 0)])
+                                                     (6, 2, 64, 0), (6, 1, 128, 0),
+                                                     (8, 2, 256, 0), (8, 1, 256, 5)])
 def test_fused_other_geometries(board, blocks, filters, gpw):
     """The C3 trunk shape (128 filters, one board per pass; with the default queue groups and
-    with bench.py's C3 groups of 16, play_group -16) and the packed 6x6 geometry (C5)."""
+    with bench.py's C3 groups of 16, play_group -16), the packed 6x6 geometry (C5) and the
+    256-filter trunk (k_play<256, 1, 4, 4, 8, 1>, one workgroup per CU; queue and static)."""
     net = _net(board, blocks, filters, seed=1)
     # three (8x8) / four (6x6) leaf batches: the visits spread over two or three root children,
     # so the games diverge (with two batches every slot plays one game, mcts.py:96-97)
@@ -136,7 +138,7 @@ def test_fused_graph_capture_and_errors():
         eng.play(run.evaluator, 1, 1.0, run.seeds, G, run._plies, run._done)
 
 
-@pytest.mark.parametrize("board,filters", [(8, 64), (6, 64), (8, 128)])
+@pytest.mark.parametrize("board,filters", [(8, 64), (6, 64), (8, 128), (8, 256)])
 def test_fused_ranged_rerun_is_per_board(board, filters):
     """The activation range's re-run inside k_play (h2_pass: an unscaled trunk, then the boards
     that overflowed again with their images scaled) keeps every board's outputs a function of
