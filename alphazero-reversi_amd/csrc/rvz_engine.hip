@@ -1892,7 +1892,7 @@ int rvz_play(rvz_engine* e, const rvz_play_args* a) {
     pa.q_next = queue ? reinterpret_cast<unsigned*>(sc) : nullptr;
     pa.q_done = queue ? reinterpret_cast<unsigned*>(sc) + 4 : nullptr;
     pa.n_groups = 0;
-    // the per-XCD pass gate (rvz_play.hip.h play_gate, rvz_play_gate; the 10x128 form only, queue
+    // the per-XCD pass gate (rvz_play.hip.h play_gate, rvz_play_gate; 8x8 at 128 / 256 filters, queue
     // schedule only: its words are zeroed with the queue's)
     pa.gate = queue ? reinterpret_cast<unsigned long long*>(sc + 4 + play_al4(G)) : nullptr;
     {   // rvz_play_gate's setting (default: RVZ_PLAY_GATE_DEFAULT), RVZ_PLAY_GATE overriding it

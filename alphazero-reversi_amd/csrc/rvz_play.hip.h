@@ -233,7 +233,7 @@ __device__ __forceinline__ int tab_insert(const PlayArgs& a, uint32_t gen, uint6
     return 0;
 }
 
-// ---- the per-XCD pass gate (rvz_play_gate; the 10x128 form) ---------------------------------
+// ---- the per-XCD pass gate (rvz_play_gate; 8x8 at 128 and 256 filters) ---------------------
 // At 10x128 every trunk pass streams the whole 11.8 MB of f16-pair weights, and the 64 workgroups
 // of an XCD, each at its own layer, keep all of it live in a 4 MB L2 (45% L2 hits,
 // the fabric path full, the clock held at 1.55 GHz). The gate makes a workgroup about to start a
@@ -241,7 +241,8 @@ __device__ __forceinline__ int tab_insert(const PlayArgs& a, uint32_t gen, uint6
 // XCD's passes start in one cohort whose members read the same layer's weights at the same time;
 // a workgroup arriving shortly after a round opened (a search phase made it late) joins that
 // cohort at once instead of waiting for the next. Timing only: the games do not depend on it. One
-// lane; no data is handed over, so no fences.
+// lane; no data is handed over, so no fences. At 256 filters (47 MB per pass at 10 blocks, one
+// workgroup per CU) the same cohorts are worth +10%.
 // An XCD's line: word 0 {round:32 | arrivals:32}, word 1 when the current round opened
 // (s_memrealtime), word 2 the XCD's running workgroups of this launch.
 __device__ __forceinline__ void gate_open(unsigned long long* w, unsigned r) {
@@ -392,7 +393,7 @@ void k_play(PlayCtx ctx0) {
     }
     double* sp = reinterpret_cast<double*>(smem) + wave * (NPOL + 7);
     uint32_t* key = reinterpret_cast<uint32_t*>(smem + SP_BYTES) + wave * 624;
-    if constexpr (F == 128 && BS == 8) {   // the pass gate counts the XCD's running workgroups
+    if constexpr (F >= 128 && BS == 8) {   // the pass gate counts the XCD's running workgroups
         const PlayArgs& a = play_ctx().a;
         if (tid == 0 && a.gate_frac > 0) gate_running(a.gate, 1);
     }
@@ -620,7 +621,7 @@ void k_play(PlayCtx ctx0) {
             for (int p0 = 0; p0 < nq; p0 += NBOARD) {
                 // the per-XCD pass gate (rvz_play_gate: on by default; built into the 10x128
                 // form only)
-                if constexpr (F == 128 && BS == 8) {
+                if constexpr (F >= 128 && BS == 8) {
                     if (play_ctx().a.gate_frac > 0) {
                         if (tid == 0) {
                             const PlayArgs& a = play_ctx().a;
@@ -689,7 +690,7 @@ void k_play(PlayCtx ctx0) {
             }
         }
     }
-    if constexpr (F == 128 && BS == 8) {   // no more passes from this workgroup
+    if constexpr (F >= 128 && BS == 8) {   // no more passes from this workgroup
         const PlayArgs& a = play_ctx().a;
         if (tid == 0 && a.gate_frac > 0) gate_running(a.gate, -1);
     }

@@ -335,7 +335,7 @@ class Engine:
         self.table_slots = int(slots)
 
     def play_gate(self, fraction: float = -1.0, timeout_us: float = 0.0, late_us: float = 0.0):
-        """rvz_play_gate: the per-XCD pass gate of play()'s 10x128 form (fraction 0: off; < 0:
+        """rvz_play_gate: the per-XCD pass gate of play()'s 8x8 forms of 128 / 256 filters (fraction 0: off; < 0:
         the default 0.8 / 400 us / 200 us). Timing only: the same games with any setting."""
         self._call("rvz_play_gate", float(fraction), float(timeout_us), float(late_us))
 

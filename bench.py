@@ -938,7 +938,7 @@ def selfplay(args, device, rank, world, full=True):
            "host_enqueue_ms_per_step": round((t_enq[-1] - t0) / max(1, args.steps) * 1e3, 3),
            "plies_per_graph": ppg,
            "play_group": args.play_group if args.fused else None,
-           "play_gate": (args.play_gate if args.fused and args.filters == 128 and args.board == 8
+           "play_gate": (args.play_gate if args.fused and args.filters >= 128 and args.board == 8
                          else None),
            "warmup_plies": {"stagger_mean": round(stagger_plies, 2),
                             "stagger": None if args.no_stagger else

@@ -251,15 +251,16 @@ int rvz_play(rvz_engine *e, const rvz_play_args *a);
  * before capturing). 8-byte {datum, generation} granules written and read with agent-scope
  * accesses, so workgroups on every XCD share it without fences. Not inside a search. */
 int rvz_play_table(rvz_engine *e, int64_t slots, int32_t max_discs);
-/* The per-XCD pass gate of rvz_play's 10x128 form (filters 128 on 8x8; the task-queue schedule).
- * At that size every trunk pass streams the whole f16-pair weight set (11.8 MB), which the
+/* The per-XCD pass gate of rvz_play's 8x8 forms of 128 and 256 filters (the task-queue schedule).
+ * There every trunk pass streams the whole f16-pair weight set (10x128: 11.8 MB), which the
  * workgroups of an XCD, each at its own layer, cannot share through the XCD's 4 MB L2. With the
  * gate a workgroup about to start a pass waits until `fraction` of its XCD's running workgroups
  * have arrived or `timeout_us` has passed since its own arrival, so the XCD's passes start
  * together and read each layer's weights together; a workgroup arriving within `late_us` of the
  * latest round's opening joins that round at once. Timing only: games, moves and counters are
  * identical with any setting (tests/test_gpu_play.py). fraction 0 turns it off; fraction < 0
- * restores the default (0.8, 400 us, 200 us: C3 +8-10% on MI355X). The environment
+ * restores the default (0.8, 400 us, 200 us: C3 +8-10% on MI355X, C3's workload at 10x256
+ * +10%). The environment
  * variable RVZ_PLAY_GATE="fraction,us[,late_us]" overrides the setting (experiments). */
 int rvz_play_gate(rvz_engine *e, double fraction, double timeout_us, double late_us);
 

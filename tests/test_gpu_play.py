@@ -201,14 +201,17 @@ def test_fused_ranged_rerun_is_per_board(board, filters):
         assert not r.evaluator.overflowed()
 
 
-@pytest.mark.parametrize("gate", [(-1.0, 0.0, 0.0), (0.05, 20.0, 0.0), (1.0, 5.0, 0.0),
-                                  (0.5, 20.0, 10.0)], ids=["default", "low", "timeout", "late"])
-def test_pass_gate_keeps_the_games(gate):
-    """The per-XCD pass gate (rvz_play_gate, rvz_play.hip.h play_gate; the 10x128 form) changes
-    when a workgroup starts a trunk pass, never what it computes: the same games with the gate
-    off and with the default setting (on), rounds opened by a low arrival fraction, by the timeout
-    (every running workgroup of an XCD never arrives together), and with the late-join window."""
-    net = _net(8, 2, 128, seed=1)
+@pytest.mark.parametrize("gate,filters", [((-1.0, 0.0, 0.0), 128), ((0.05, 20.0, 0.0), 128),
+                                          ((1.0, 5.0, 0.0), 128), ((0.5, 20.0, 10.0), 128),
+                                          ((-1.0, 0.0, 0.0), 256)],
+                         ids=["default", "low", "timeout", "late", "default-256"])
+def test_pass_gate_keeps_the_games(gate, filters):
+    """The per-XCD pass gate (rvz_play_gate, rvz_play.hip.h play_gate; the 8x8 forms of 128 and
+    256 filters) changes when a workgroup starts a trunk pass, never what it computes: the same
+    games with the gate off and with the default setting (on), rounds opened by a low arrival
+    fraction, by the timeout (every running workgroup of an XCD never arrives together), and with
+    the late-join window."""
+    net = _net(8, 2, filters, seed=1)
     G, S, plies = 160, 200, 12
     a = _fused(net, G, S, plies, True, True, gpw=-4, gate=(0.0, 0.0, 0.0))
     b = _fused(net, G, S, plies, True, True, gpw=-4, gate=gate)
