@@ -112,3 +112,22 @@ def test_evaluator_entry_points_reject_a_misaligned_workspace():
         assert lib.rvz_resnet_heads_fc(8, work, 64, params, 64, 6, out, out, None) == EINVAL
         assert lib.rvz_resnet_fwd_h2(8, x, 64, params, blob, 64, 6, work, out, out,
                                      None) == EINVAL
+
+
+def test_evaluator_width_rules_without_gpu():
+    """The h2 widths at the C-ABI (argument checks only, no HIP call): 64 and 128 filters on both
+    boards, 256 on 8x8; anything else is RVZ_EINVAL. rvz_resnet_h2_grid: one workgroup per board
+    at 128 / 256 on 8x8 (two boards per unit at 64), plus 1/8 spare workgroups rounded to 8."""
+    import rvz
+    lib = rvz.load()
+    EINVAL = -22
+    assert lib.rvz_resnet_h2_grid(8, 256, 10) == 18 and lib.rvz_resnet_h2_grid(8, 128, 10) == 18
+    assert lib.rvz_resnet_h2_grid(8, 64, 10) == 13
+    for board, f in ((6, 256), (8, 192), (8, 32), (8, 512), (7, 64)):
+        assert lib.rvz_resnet_h2_grid(board, f, 10) == EINVAL, (board, f)
+    for f in (64, 128, 256):
+        assert lib.rvz_resnet_h2_size(f, 3) > 0 and lib.rvz_resnet_params_size(8, f, 3) > 0
+    assert lib.rvz_resnet_h2_size(192, 3) == EINVAL
+    # a 6x6 trunk at 256 filters is refused before anything is launched
+    p = 0x10000
+    assert lib.rvz_resnet_trunk_h2(6, p, 4, p, p, 256, 1, p, None) == EINVAL
