@@ -53,6 +53,9 @@ typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 #ifndef RVZ_H2_APD
 #define RVZ_H2_APD 1         // activation prefetch distance, k-steps
 #endif
+#ifndef RVZ_H2_PD256
+#define RVZ_H2_PD256 1       // F = 256 (one workgroup per CU): weight prefetch distance, k-steps
+#endif
 #ifndef RVZ_H2_OCC
 #define RVZ_H2_OCC 2         // workgroups per CU the register budget is sized for
 #endif
@@ -66,7 +69,7 @@ __host__ __device__ inline int64_t h2_layer_elems(int F) { return (int64_t)9 * F
 __host__ __device__ inline int64_t h2_kstep_elems(int F) { return (int64_t)2 * F * H2_K; }
 // zero k-steps after the last layer: the weight prefetch of the next (absent) layer reads them
 __host__ __device__ inline int64_t h2_pad_ksteps(int) { return 4; }
-static_assert(RVZ_H2_PD <= 4, "prefetch stays inside the padded blob");
+static_assert(RVZ_H2_PD <= 4 && RVZ_H2_PD256 <= 4, "prefetch stays inside the padded blob");
 __host__ __device__ inline int64_t h2_stem_off(int F, int NB) {
     return 2 * NB * h2_layer_elems(F) + h2_pad_ksteps(F) * h2_kstep_elems(F);
 }
@@ -812,7 +815,7 @@ __device__ __forceinline__ RangeS<NBOARD> h2_trunk(char* smem, const float* __re
     float* xin = reinterpret_cast<float*>(actB);     // free until the first conv writes B
     const H2W wr(blob, h2_blob_elems(F, n_blocks));
     const RangeLds rl{reinterpret_cast<float*>(smem + C::RMAX)};
-    constexpr int PD = RG || F == 256 ? 1 : RVZ_H2_PD, APD = RG ? 0 : RVZ_H2_APD;
+    constexpr int PD = RG ? 1 : (F == 256 ? RVZ_H2_PD256 : RVZ_H2_PD), APD = RG ? 0 : RVZ_H2_APD;
     PASS_NOW(tp0);
     f16x8 bc[PD][CTW][2];
     if (n_blocks > 0) {
