@@ -45,11 +45,12 @@ MFMA16_PEAK_TFLOPS = 2500.0      # dense 16-bit (f16/bf16) MFMA peak, same sourc
 PRESETS = {   # BASELINE.json configs
     # lanes: independent game lanes per GPU (same games; measured best per config)
     # c1: the reference's own plumbing case (one game, 100 sims, the ModelConfig default 5x128
-    # net; config.py:14-15) on one GPU, with the CPU port on the same single game beside it
-    "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1, fused=False),
-    # fused: the fused self-play launch (k_play) measures faster at C2 (r03o: +4-5% over 2
-    # lanes); at C3 (one 27k-row trunk launch per batch, no ramp/tail to remove) and C5 (86 KB of
-    # LDS: one workgroup per CU, nothing covers the search phases) the launches are faster
+    # net; config.py:14-15) on one GPU, with the CPU port on the same single game beside it.
+    # fused: the fused self-play launch (k_play, one workgroup plays the game: no per-batch
+    # launches, and the cross-game table serves positions earlier searches evaluated) — C1
+    # 11.3k vs 8.9k pull-style (round 6, profiles/r06s_c1_fused_vs_pull.txt); C2 (r03o: +4-5%
+    # over 2 lanes), C3 and C5 since round 4 (with the table)
+    "c1": dict(games=1, sims=100, blocks=5, filters=128, board=8, lanes=1, fused=True),
     "c2": dict(games=4096, sims=800, blocks=6, filters=64, board=8, lanes=2, fused=True,
                play_group=-6),
     "c3": dict(games=32768, sims=800, blocks=10, filters=128, board=8, lanes=1, fused=True,

@@ -127,6 +127,34 @@ def test_k_play_c3_bench_form_at_full_size(oracle):
     assert not run.evaluator.overflowed()
 
 
+def test_k_play_c1_preset_vs_oracle_whole_game(oracle):
+    """C1's fused preset (round 6): one game, 100 sims, the ModelConfig default 5x128 net, the
+    memo + the last batch left to it + the cross-game table, one workgroup playing the game:
+    61 plies (a whole game of at most 60 moves, then the next one, autoreset), each ply's f64
+    policy and move equal to the oracle's; the same game, move for move, as the pull-style runner
+    (per-batch launches, no table), which the preset ran until round 6. Table hits come from
+    positions the game's earlier searches evaluated. (At 100 sims a search is two batches of 64:
+    the second goes whole to the first unvisited root child, mcts.py:96-97, so this pins the
+    launch's mechanics at C1's shape; the RNG and the net's outputs are pinned by the other
+    tests.)"""
+    import rvz
+    net = _net(8, 5, 128, seed=3)
+    G, S, plies = 1, 100, 61
+    run = _vs_oracle(oracle, net, G, S, plies, 0, sample_n=1, table=(1 << 20, 14))
+    assert int(run.eng.table_stats[0].item()) > 0
+    ref = rvz.SelfPlayRunner(rvz.Engine(G, S, 64, compact_leaves=True, memo=True),
+                             rvz.LeafEvaluator(net), autoreset=True, seed_base=42,
+                             skip_last_eval=True)
+    ref.start()
+    for _ in range(plies):
+        ref.ply()
+    for x, y in zip(run.eng.get_state(), ref.eng.get_state()):
+        assert torch.equal(x, y)
+    assert torch.equal(run._plies, ref._plies) and torch.equal(run._done, ref._done)
+    assert torch.equal(run.seeds, ref.seeds)
+    ref.eng.check()
+
+
 def test_k_play_c5_preset_equals_runner_at_full_size():
     """C5 as bench.py runs it (16,384 games, 400 sims, groups of 24, three 6x6 boards per
     workgroup), 34 plies (every 6x6 game ends within 32, so restarts are included): every ply's
