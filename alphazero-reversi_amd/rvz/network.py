@@ -191,6 +191,20 @@ class ModuleEvaluator:
     def overflowed(self) -> bool:
         return False
 
+    def bind_engine(self, engine):
+        """Called by an Engine the first time it searches with this evaluator (Engine._bind)."""
+        import weakref
+        self.__dict__.setdefault("_engines", weakref.WeakSet()).add(engine)
+
+    def refresh(self):
+        """The module's weights changed (a training step): the evaluator reads the live module,
+        so only the engines' memo links to the old net's outputs are dropped (as
+        LeafEvaluator.refresh does)."""
+        self.net.eval()
+        for eng in list(getattr(self, "_engines", ())):
+            if getattr(eng, "memo_on", False) or getattr(eng, "table_slots", 0):
+                eng.memo_reset()
+
 
 def leaf_evaluator(net: nn.Module, dtype=torch.float32, device=None):
     """The default leaf evaluator of SelfPlay / ELOPlayer: LeafEvaluator (the h2 kernels) when

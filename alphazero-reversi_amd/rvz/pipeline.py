@@ -25,7 +25,7 @@ import torch
 import torch.distributed as dist
 
 from .engine import Engine
-from .network import LeafEvaluator
+from .network import LeafEvaluator, leaf_evaluator
 from .selfplay import SelfPlayRunner
 from .trainer import DDPTrainer, records_to_training
 
@@ -52,7 +52,11 @@ class SelfPlayTrainer:
         self.trainer = DDPTrainer(model, lr=lr, weight_decay=weight_decay,
                                   gradient_clip=gradient_clip, batch_size=train_batch,
                                   lr_milestones=lr_milestones, lr_gamma=lr_gamma)
-        self.evaluator = LeafEvaluator(model)
+        # the h2 kernels when they cover the net, else the module itself on the GPU
+        # (ModuleEvaluator: pull-style, eager plies; it reads the live module, so refresh() only
+        # drops the memo)
+        self.evaluator = leaf_evaluator(model, device=self.device)
+        h2 = isinstance(self.evaluator, LeafEvaluator)
         bs = int(getattr(model, "board_size", 8))
         self.eng = Engine(games, num_simulations, batch_size, c_puct, board_size=bs,
                           device=self.device, compact_leaves=compact_leaves, memo=memo)
@@ -60,7 +64,7 @@ class SelfPlayTrainer:
         # fused: every game of the iteration in ONE rvz_play launch with device records, the
         # memo's deferred last batch and the cross-game table (a new generation per refresh());
         # else the pull-style ply graph (per-batch launches, records copied per ply)
-        self.fused = bool(fused)
+        self.fused = bool(fused) and h2
         if table_slots is None:
             table_slots = 1 << min(22, max(12, (32 * self.games - 1).bit_length()))
         if self.fused and table_slots:
@@ -69,7 +73,7 @@ class SelfPlayTrainer:
                                      max_plies=self.max_plies,
                                      seed_base=self.seed + self.rank * self.games,
                                      fused=self.fused, skip_last_eval=self.fused and memo)
-        self.graph = bool(graph)
+        self.graph = bool(graph) and h2
         self.iteration = 0
 
     def _seeds(self):

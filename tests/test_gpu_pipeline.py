@@ -74,6 +74,37 @@ def test_c4_shaped_iteration_over_rccl_world1(tmp_path):
     assert torch.equal(t["value_targets"], data["value_targets"])
 
 
+def test_pipeline_with_a_net_the_h2_kernels_do_not_cover(tmp_path):
+    """SelfPlayTrainer with a 32-filter net (the reference's pipeline takes any num_filters,
+    network.py:33): its evaluator is the module on the GPU (ModuleEvaluator, with a warning), the
+    plies run pull-style and eager, training changes the weights, and the next iteration's games
+    (the evaluator reads the live module; refresh() drops the memo) equal an eager SelfPlay of the
+    trained net with the same seeds."""
+    import rvz
+    from rvz.pipeline import SelfPlayTrainer
+    G, S = 64, 200          # four batches: the games differ
+    torch.manual_seed(2)
+    net = rvz.AlphaZeroNetwork(8, 2, 32).cuda()
+    init = {k: v.clone() for k, v in net.state_dict().items()}
+    with pytest.warns(UserWarning, match="ModuleEvaluator"):
+        spt = SelfPlayTrainer(net, G, num_simulations=S, seed=11, train_steps=5, train_batch=64)
+    assert isinstance(spt.evaluator, rvz.ModuleEvaluator) and not spt.fused and not spt.graph
+    r0 = spt.run_iteration()
+    assert r0["board_steps"] == r0["samples"] >= 9 * G and np.isfinite(r0["train/loss"])
+    moved = max((net.state_dict()[k].float() - init[k].float()).abs().max().item()
+                for k in init if init[k].is_floating_point())
+    assert moved > 1e-4
+    data = spt.generate()                       # iteration 1, the trained net
+    with pytest.warns(UserWarning, match="ModuleEvaluator"):
+        sp = rvz.SelfPlay(net, {"num_simulations": S, "seed": 11 + G, "save_dir": str(tmp_path)})
+    games = sp.generate_games(G)
+    assert len({g["states"][4].tobytes() for g in games}) > 1
+    t = sp.training_tensors()
+    assert torch.equal(t["states"], data["states"])
+    assert torch.equal(t["policy_targets"], data["policy_targets"])
+    assert torch.equal(t["value_targets"], data["value_targets"])
+
+
 def test_ddp_trainer_over_rccl_world1_equals_plain_training():
     """DDPTrainer with a torch.distributed process group on the 'nccl' backend (RCCL on ROCm) at
     world size 1: every step's gradients go through DDP's bucketed RCCL all-reduce, and the
