@@ -74,28 +74,38 @@ def test_c4_shaped_iteration_over_rccl_world1(tmp_path):
     assert torch.equal(t["value_targets"], data["value_targets"])
 
 
-def test_pipeline_with_a_net_the_h2_kernels_do_not_cover(tmp_path):
-    """SelfPlayTrainer with a 32-filter net (the reference's pipeline takes any num_filters,
-    network.py:33): its evaluator is the module on the GPU (ModuleEvaluator, with a warning), the
-    plies run pull-style and eager, training changes the weights, and the next iteration's games
-    (the evaluator reads the live module; refresh() drops the memo) equal an eager SelfPlay of the
-    trained net with the same seeds."""
+@pytest.mark.parametrize("filters", [32, 256])
+def test_pipeline_with_other_net_widths(tmp_path, filters):
+    """SelfPlayTrainer with a 32- and a 256-filter net (the reference's pipeline takes any
+    num_filters, network.py:33). 32: the h2 kernels do not cover it, so the evaluator is the
+    module on the GPU (ModuleEvaluator, with a warning), the plies run pull-style and eager;
+    256: the h2 kernels and the fused launch with the table. Training changes the weights, and the
+    next iteration's games (ModuleEvaluator reads the live module, LeafEvaluator re-reads the
+    weights; refresh() drops the memo / table) equal an eager SelfPlay of the trained net with the
+    same seeds."""
+    import contextlib
     import rvz
     from rvz.pipeline import SelfPlayTrainer
     G, S = 64, 200          # four batches: the games differ
     torch.manual_seed(2)
-    net = rvz.AlphaZeroNetwork(8, 2, 32).cuda()
+    net = rvz.AlphaZeroNetwork(8, 2, filters).cuda()
     init = {k: v.clone() for k, v in net.state_dict().items()}
-    with pytest.warns(UserWarning, match="ModuleEvaluator"):
+    module = filters == 32
+    warn = (lambda: pytest.warns(UserWarning, match="ModuleEvaluator")) if module else \
+        contextlib.nullcontext
+    with warn():
         spt = SelfPlayTrainer(net, G, num_simulations=S, seed=11, train_steps=5, train_batch=64)
-    assert isinstance(spt.evaluator, rvz.ModuleEvaluator) and not spt.fused and not spt.graph
+    if module:
+        assert isinstance(spt.evaluator, rvz.ModuleEvaluator) and not spt.fused and not spt.graph
+    else:
+        assert isinstance(spt.evaluator, rvz.LeafEvaluator) and spt.fused
     r0 = spt.run_iteration()
     assert r0["board_steps"] == r0["samples"] >= 9 * G and np.isfinite(r0["train/loss"])
     moved = max((net.state_dict()[k].float() - init[k].float()).abs().max().item()
                 for k in init if init[k].is_floating_point())
     assert moved > 1e-4
     data = spt.generate()                       # iteration 1, the trained net
-    with pytest.warns(UserWarning, match="ModuleEvaluator"):
+    with warn():
         sp = rvz.SelfPlay(net, {"num_simulations": S, "seed": 11 + G, "save_dir": str(tmp_path)})
     games = sp.generate_games(G)
     assert len({g["states"][4].tobytes() for g in games}) > 1
