@@ -619,8 +619,8 @@ void k_play(PlayCtx ctx0) {
 
             // evaluation phase: the trunk over the queued rows, NBOARD boards per pass
             for (int p0 = 0; p0 < nq; p0 += NBOARD) {
-                // the per-XCD pass gate (rvz_play_gate: on by default; built into the 10x128
-                // form only)
+                // the per-XCD pass gate (rvz_play_gate: on by default; built into the 8x8 forms
+                // at 128 and 256 filters)
                 if constexpr (F >= 128 && BS == 8) {
                     if (play_ctx().a.gate_frac > 0) {
                         if (tid == 0) {
